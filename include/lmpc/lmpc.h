@@ -1,0 +1,179 @@
+/*
+ * lmpc.h -- C-ABI of the MI355X-native batched convex-MPC GRF QP solver.
+ *
+ * This is the drop-in boundary for the reference's convex-MPC QP path
+ * (zha0ming1e/legged_mpc_control, src/legged_ctrl):
+ *
+ *   reference interface (file:line, relative to src/legged_ctrl)        replaced by
+ *   ---------------------------------------------------------------     -----------------------
+ *   ConvexQPSolver(q_weights, r_weights)  ConvexQPSolver.h:25 /         lmpc_create
+ *       ConvexQPSolver.cpp:16-196 (OSQP setup, constants mu/f_max/g)
+ *   ~ConvexQPSolver / OSQP workspace       ConvexQPSolver.h:62          lmpc_destroy
+ *   calc_mpc_reference(state, leg_FSM)     ConvexQPSolver.cpp:254-313   lmpc_pack_record +
+ *                                                                       lmpc_contact_schedule
+ *   update_bound_constraints(...)          ConvexQPSolver.cpp:329-346   lmpc_contact_schedule
+ *   LeggedContactFSM::predict_contact_state LeggedContactFSM.cpp:280-294 lmpc_predict_contact
+ *   update_cons_matrix()                   ConvexQPSolver.cpp:230-239   (no-op: matrices are
+ *                                                                        built on the device)
+ *   compute_grfs(state) -> u_0 (12)        ConvexQPSolver.cpp:314-327   lmpc_solve_batch (host
+ *                                                                        buffers, batch >= 1) /
+ *                                                                        lmpc_solve_batch_device
+ *
+ * All arithmetic is fp64, as in the reference (Eigen double).  Plain C types
+ * only; no exceptions cross this boundary.  A context is NOT thread-safe
+ * (like the reference solver object): use one context per host thread.
+ *
+ * Per-instance record layout (doubles, see lmpc_record_len):
+ *   [ x0(12) | rot(9, row-major body->world) | feet(4 legs x xyz, world-aligned,
+ *     body-centred = foot_pos_abs) | x_ref(H x 12) ]
+ *   x0    = [euler(3), pos(3), omega_world(3), v_world(3)]  (ConvexQPSolver.cpp:256-259)
+ *   x_ref = reference state of step i (ConvexQPSolver.cpp:264-276)
+ * contact[H][4] (uint8, 1 = stance): step 0 = plan_contacts, step i>=1 =
+ *   predict_contact_state(i*dt) (ConvexQPSolver.cpp:329-346).
+ * Output grf[H][12]: u_0..u_{H-1}, FL,FR,RL,RR x (fx,fy,fz) in the world frame;
+ *   grf[0..11] is exactly what compute_grfs returns.
+ */
+#ifndef LMPC_LMPC_H
+#define LMPC_LMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LMPC_ABI_VERSION 1
+#define LMPC_MAX_HORIZON 32
+
+/* return codes (API level) */
+#define LMPC_OK 0
+#define LMPC_ERR_ARG (-1)
+#define LMPC_ERR_DEVICE (-2)
+#define LMPC_ERR_ALLOC (-3)
+#define LMPC_ERR_LAUNCH (-4)
+#define LMPC_ERR_NOT_BUILT (-5)
+
+/* per-QP status codes (status[b]) */
+#define LMPC_QP_CONVERGED 0
+#define LMPC_QP_MAX_ITER 1 /* best iterate returned */
+#define LMPC_QP_NAN 2      /* zeros returned, as the reference does (ConvexQPSolver.cpp:321-326) */
+
+#define LMPC_REC_X0 0
+#define LMPC_REC_ROT 12
+#define LMPC_REC_FEET 21
+#define LMPC_REC_XREF 33
+
+/* Shared parameters: LeggedParam fields read by the path (LeggedState.h:156-165)
+ * plus the constants the reference hard-codes (ConvexQPSolver.cpp:25,26,171,175). */
+typedef struct lmpc_params {
+    double q_weights[12];
+    double r_weights[12];
+    double robot_mass;
+    double trunk_inertia[9]; /* row-major, body frame */
+    double mu;               /* friction coefficient, reference 0.3 */
+    double f_max;            /* normal-force bound, reference 180 N */
+    double gravity;          /* reference 9.8 */
+    double dt;               /* MPC step, reference MPC_UPDATE_FREQUENCY/1000 = 0.01 s */
+} lmpc_params;
+
+/* Solver options (defaults via lmpc_options_default).  The device solve is a
+ * Mehrotra interior point whose Newton step is a Riccati (LQR) recursion over
+ * the horizon, followed by an active-set polish (equality-constrained LQR on
+ * the identified active set, verified by primal feasibility and multiplier
+ * signs).  A verified polish is the exact optimum of the reference's QP. */
+typedef struct lmpc_options {
+    int max_iter;     /* IPM iterations cap per attempt (default 40) */
+    int max_rounds;   /* active-set polish rounds per attempt (default 4) */
+    int max_attempts; /* IPM+polish attempts; tol_mu x1e-3 each retry (default 3) */
+    double tol_mu;    /* IPM stop: mean complementarity (default 1e-8) */
+    double tol_p;     /* polish primal feasibility, relative to f_max (default 1e-9) */
+    double tol_d;     /* polish multiplier sign, relative to gradient scale (default 1e-9) */
+} lmpc_options;
+
+/* Robot presets: gazebo_go1_convex.yaml:39-71 (+ LeggedState.cpp:146,155-160
+ * defaults for mass/inertia) and gazebo_a1_convex.yaml:40-72,133-140. */
+void lmpc_params_go1(lmpc_params* p);
+void lmpc_params_a1(lmpc_params* p);
+void lmpc_options_default(lmpc_options* o);
+
+int lmpc_record_len(int horizon); /* doubles per record: 33 + 12*H */
+int lmpc_abi_version(void);
+const char* lmpc_strerror(int code);
+
+/* ---- device solver ---------------------------------------------------- */
+typedef struct lmpc_ctx lmpc_ctx;
+
+/* Creates a solver context on HIP device `device` for horizon H (1..LMPC_MAX_HORIZON)
+ * and batches up to max_batch (host-pointer path staging buffers). */
+int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lmpc_ctx** out);
+void lmpc_destroy(lmpc_ctx* ctx);
+int lmpc_set_options(lmpc_ctx* ctx, const lmpc_options* o);
+int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
+
+/* Host buffers in/out, synchronous.  rec[batch][33+12H], contact[batch][H][4],
+ * grf[batch][H][12]; status[batch] and iters[batch] may be NULL. */
+int lmpc_solve_batch(lmpc_ctx* ctx, const double* rec, const uint8_t* contact, int batch,
+                     double* grf, int32_t* status, int32_t* iters);
+
+/* Device buffers (already resident in HBM), asynchronous on `stream`
+ * (a hipStream_t; NULL = the context's own stream). status/iters may be NULL. */
+int lmpc_solve_batch_device(lmpc_ctx* ctx, const double* d_rec, const uint8_t* d_contact,
+                            int batch, double* d_grf, int32_t* d_status, int32_t* d_iters,
+                            void* stream);
+
+/* Synchronise the context's stream. */
+int lmpc_sync(lmpc_ctx* ctx);
+
+/* ---- host-side path helpers (exact restatements of the reference) ------ */
+
+/* LeggedContactFSM gait tables (LeggedContactFSM.cpp:93-212). */
+#define LMPC_GAIT_TROT 0
+#define LMPC_GAIT_CRAWL 1
+#define LMPC_GAIT_TROT_WITH_STAND 2
+#define LMPC_GAIT_STAND 3
+
+/* predict_contact_state (LeggedContactFSM.cpp:280-294): 1 = STANCE, 0 = SWING */
+int lmpc_predict_contact(int gait, int leg, double gait_phase, double gait_speed, double dt);
+/* FSM state once it has advanced to gait_phase (get_contact_state()). */
+int lmpc_current_contact(int gait, int leg, double gait_phase);
+
+/* update_bound_constraints schedule (ConvexQPSolver.cpp:329-346):
+ * contact[0][j] = plan_contacts[j]; contact[i][j] = predict(gait, j, phase, speed, i*dt). */
+int lmpc_contact_schedule(int gait, double gait_phase, double gait_speed, double dt, int horizon,
+                          const uint8_t plan_contacts[4], uint8_t* contact);
+
+/* calc_mpc_reference input packing (ConvexQPSolver.cpp:256-276). */
+typedef struct lmpc_state_in {
+    double root_euler[3];
+    double root_pos[3];
+    double root_ang_vel[3];   /* world frame */
+    double root_lin_vel[3];   /* world frame */
+    double root_rot_mat[9];   /* row-major */
+    double foot_pos_abs[12];  /* leg-major xyz */
+    double root_euler_d[3];
+    double root_pos_d[3];
+    double root_lin_vel_d_rel[3];
+    double root_ang_vel_d_rel[3];
+} lmpc_state_in;
+/* Writes the record; also returns v_d_world = R * v_d_rel (reference writes it
+ * back into state.ctrl.root_lin_vel_d_world, ConvexQPSolver.cpp:260). */
+int lmpc_pack_record(const lmpc_params* p, int horizon, const lmpc_state_in* st, double* rec,
+                     double lin_vel_d_world[3]);
+
+/* ---- synthetic batches, counter-based (Philox4x32-10) ---- */
+typedef struct lmpc_synth_cfg {
+    int gait;             /* LMPC_GAIT_*, or -1 = mixed (uniform over the four) */
+    double gait_speed;    /* phase per second (Go1 4.0, A1 3.5) */
+    double default_feet[12]; /* default_foot_pos_rel, leg-major */
+    int standing;         /* 1 = config-1 nominal standing instance (no randomness) */
+} lmpc_synth_cfg;
+void lmpc_synth_cfg_go1(lmpc_synth_cfg* c);
+void lmpc_synth_cfg_a1_standing(lmpc_synth_cfg* c);
+/* Instance b of the batch is global index first_index+b; identical on every rank. */
+int lmpc_synth_fill(const lmpc_params* p, const lmpc_synth_cfg* cfg, int horizon, uint64_t seed,
+                    int64_t first_index, int count, double* rec, uint8_t* contact);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LMPC_LMPC_H */

@@ -1,0 +1,144 @@
+"""ctypes binding of the C-ABI in include/lmpc/lmpc.h (liblmpc.so, built in-tree).
+
+The product path has no fallback: if the HIP library is missing or the device
+code cannot run, calls raise instead of silently computing on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "liblmpc.so")
+
+LMPC_OK = 0
+LMPC_QP_CONVERGED = 0
+LMPC_QP_MAX_ITER = 1
+LMPC_QP_NAN = 2
+LMPC_MAX_HORIZON = 32
+GAIT_TROT, GAIT_CRAWL, GAIT_TROT_WITH_STAND, GAIT_STAND = 0, 1, 2, 3
+
+# every symbol include/lmpc/lmpc.h declares (checked by tests/test_capi.py)
+EXPORTED_SYMBOLS = (
+    "lmpc_params_go1", "lmpc_params_a1", "lmpc_options_default", "lmpc_record_len",
+    "lmpc_abi_version", "lmpc_strerror", "lmpc_create", "lmpc_destroy", "lmpc_set_options",
+    "lmpc_set_params", "lmpc_solve_batch", "lmpc_solve_batch_device", "lmpc_sync",
+    "lmpc_predict_contact", "lmpc_current_contact", "lmpc_contact_schedule", "lmpc_pack_record",
+    "lmpc_synth_cfg_go1", "lmpc_synth_cfg_a1_standing", "lmpc_synth_fill",
+)
+
+
+class LmpcParams(ctypes.Structure):
+    _fields_ = [
+        ("q_weights", ctypes.c_double * 12),
+        ("r_weights", ctypes.c_double * 12),
+        ("robot_mass", ctypes.c_double),
+        ("trunk_inertia", ctypes.c_double * 9),
+        ("mu", ctypes.c_double),
+        ("f_max", ctypes.c_double),
+        ("gravity", ctypes.c_double),
+        ("dt", ctypes.c_double),
+    ]
+
+
+class LmpcOptions(ctypes.Structure):
+    _fields_ = [
+        ("max_iter", ctypes.c_int),
+        ("max_rounds", ctypes.c_int),
+        ("max_attempts", ctypes.c_int),
+        ("tol_mu", ctypes.c_double),
+        ("tol_p", ctypes.c_double),
+        ("tol_d", ctypes.c_double),
+    ]
+
+
+class LmpcStateIn(ctypes.Structure):
+    _fields_ = [
+        ("root_euler", ctypes.c_double * 3),
+        ("root_pos", ctypes.c_double * 3),
+        ("root_ang_vel", ctypes.c_double * 3),
+        ("root_lin_vel", ctypes.c_double * 3),
+        ("root_rot_mat", ctypes.c_double * 9),
+        ("foot_pos_abs", ctypes.c_double * 12),
+        ("root_euler_d", ctypes.c_double * 3),
+        ("root_pos_d", ctypes.c_double * 3),
+        ("root_lin_vel_d_rel", ctypes.c_double * 3),
+        ("root_ang_vel_d_rel", ctypes.c_double * 3),
+    ]
+
+
+class LmpcSynthCfg(ctypes.Structure):
+    _fields_ = [
+        ("gait", ctypes.c_int),
+        ("gait_speed", ctypes.c_double),
+        ("default_feet", ctypes.c_double * 12),
+        ("standing", ctypes.c_int),
+    ]
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    """Load liblmpc.so (raises NativeLibraryError if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, dp, i32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        pp = ctypes.POINTER(LmpcParams)
+        L.lmpc_params_go1.argtypes = [pp]
+        L.lmpc_params_a1.argtypes = [pp]
+        L.lmpc_options_default.argtypes = [ctypes.POINTER(LmpcOptions)]
+        L.lmpc_record_len.argtypes = [ctypes.c_int]
+        L.lmpc_record_len.restype = ctypes.c_int
+        L.lmpc_abi_version.restype = ctypes.c_int
+        L.lmpc_strerror.argtypes = [ctypes.c_int]
+        L.lmpc_strerror.restype = ctypes.c_char_p
+        L.lmpc_create.argtypes = [pp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.lmpc_create.restype = ctypes.c_int
+        L.lmpc_destroy.argtypes = [vp]
+        L.lmpc_destroy.restype = None
+        L.lmpc_set_options.argtypes = [vp, ctypes.POINTER(LmpcOptions)]
+        L.lmpc_set_options.restype = ctypes.c_int
+        L.lmpc_set_params.argtypes = [vp, pp]
+        L.lmpc_set_params.restype = ctypes.c_int
+        L.lmpc_solve_batch.argtypes = [vp, dp, u8p, ctypes.c_int, dp, i32p, i32p]
+        L.lmpc_solve_batch.restype = ctypes.c_int
+        L.lmpc_solve_batch_device.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
+        L.lmpc_solve_batch_device.restype = ctypes.c_int
+        L.lmpc_sync.argtypes = [vp]
+        L.lmpc_sync.restype = ctypes.c_int
+        L.lmpc_predict_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double]
+        L.lmpc_predict_contact.restype = ctypes.c_int
+        L.lmpc_current_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
+        L.lmpc_current_contact.restype = ctypes.c_int
+        L.lmpc_contact_schedule.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, u8p, u8p]
+        L.lmpc_contact_schedule.restype = ctypes.c_int
+        L.lmpc_pack_record.argtypes = [pp, ctypes.c_int, ctypes.POINTER(LmpcStateIn), dp, dp]
+        L.lmpc_pack_record.restype = ctypes.c_int
+        L.lmpc_synth_cfg_go1.argtypes = [ctypes.POINTER(LmpcSynthCfg)]
+        L.lmpc_synth_cfg_a1_standing.argtypes = [ctypes.POINTER(LmpcSynthCfg)]
+        L.lmpc_synth_fill.argtypes = [pp, ctypes.POINTER(LmpcSynthCfg), ctypes.c_int, ctypes.c_uint64,
+                                      ctypes.c_int64, ctypes.c_int, dp, u8p]
+        L.lmpc_synth_fill.restype = ctypes.c_int
+        if L.lmpc_abi_version() != 1:
+            raise NativeLibraryError("liblmpc.so ABI version mismatch")
+        _lib = L
+        return L
+
+
+def check(rc: int, what: str = "lmpc") -> None:
+    if rc != LMPC_OK:
+        raise RuntimeError(f"{what} failed: {lib().lmpc_strerror(rc).decode()} ({rc})")

@@ -1,0 +1,182 @@
+// lmpc_capi.cpp -- C-ABI (include/lmpc/lmpc.h) over the HIP solve kernel.
+//
+// Replaces the reference's ConvexQPSolver/OSQP object lifetime
+// (ConvexQPSolver.cpp:16-196 construction, :314-327 compute_grfs):
+// a context owns the device staging buffers and a HIP stream; callers own
+// their host buffers; nothing is retained after a call returns.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+
+#include "lmpc/lmpc.h"
+#include "lmpc_device.h"
+
+namespace lmpc {
+hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, int batch, double* grf,
+                     int32_t* status, int32_t* iters, hipStream_t stream);
+}
+
+struct lmpc_ctx {
+    int device = 0;
+    int H = 0;
+    int max_batch = 0;
+    lmpc::DevParams prm{};
+    hipStream_t stream = nullptr;
+    double* d_rec = nullptr;
+    uint8_t* d_contact = nullptr;
+    double* d_grf = nullptr;
+    int32_t* d_status = nullptr;
+    int32_t* d_iters = nullptr;
+};
+
+namespace {
+
+void fill_params(lmpc::DevParams& d, const lmpc_params* p) {
+    for (int i = 0; i < 12; ++i) {
+        d.q[i] = p->q_weights[i];
+        d.r[i] = p->r_weights[i];
+    }
+    d.mass = p->robot_mass;
+    for (int i = 0; i < 9; ++i) d.Ib[i] = p->trunk_inertia[i];
+    d.mu = p->mu;
+    d.fmax = p->f_max;
+    d.grav = p->gravity;
+    d.dt = p->dt;
+}
+
+void fill_options(lmpc::DevParams& d, const lmpc_options* o) {
+    d.max_iter = o->max_iter;
+    d.max_rounds = o->max_rounds;
+    d.max_attempts = o->max_attempts;
+    d.tol_mu = o->tol_mu;
+    d.tol_p = o->tol_p;
+    d.tol_d = o->tol_d;
+}
+
+bool params_ok(const lmpc_params* p) {
+    if (!p) return false;
+    if (!(p->robot_mass > 0.0) || !(p->dt > 0.0) || !(p->mu > 0.0) || !(p->f_max >= 0.0)) return false;
+    for (int i = 0; i < 12; ++i)
+        if (!(p->r_weights[i] > 0.0) || !(p->q_weights[i] >= 0.0)) return false;  // R > 0: strictly convex
+    return true;
+}
+
+void free_bufs(lmpc_ctx* c) {
+    hipFree(c->d_rec);
+    hipFree(c->d_contact);
+    hipFree(c->d_grf);
+    hipFree(c->d_status);
+    hipFree(c->d_iters);
+    c->d_rec = nullptr;
+    c->d_contact = nullptr;
+    c->d_grf = nullptr;
+    c->d_status = nullptr;
+    c->d_iters = nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lmpc_ctx** out) {
+    if (!out || !params_ok(p) || horizon < 1 || horizon > LMPC_MAX_HORIZON || max_batch < 0) return LMPC_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LMPC_ERR_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return LMPC_ERR_DEVICE;
+    lmpc_ctx* c = new (std::nothrow) lmpc_ctx();
+    if (!c) return LMPC_ERR_ALLOC;
+    c->device = device;
+    c->H = horizon;
+    c->max_batch = max_batch;
+    fill_params(c->prm, p);
+    lmpc_options o;
+    lmpc_options_default(&o);
+    fill_options(c->prm, &o);
+    c->prm.H = horizon;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return LMPC_ERR_DEVICE;
+    }
+    if (max_batch > 0) {
+        const size_t rl = (size_t)lmpc_record_len(horizon);
+        bool ok = hipMalloc(&c->d_rec, (size_t)max_batch * rl * sizeof(double)) == hipSuccess &&
+                  hipMalloc(&c->d_contact, (size_t)max_batch * 4 * horizon) == hipSuccess &&
+                  hipMalloc(&c->d_grf, (size_t)max_batch * 12 * horizon * sizeof(double)) == hipSuccess &&
+                  hipMalloc(&c->d_status, (size_t)max_batch * sizeof(int32_t)) == hipSuccess &&
+                  hipMalloc(&c->d_iters, (size_t)max_batch * sizeof(int32_t)) == hipSuccess;
+        if (!ok) {
+            free_bufs(c);
+            hipStreamDestroy(c->stream);
+            delete c;
+            return LMPC_ERR_ALLOC;
+        }
+    }
+    *out = c;
+    return LMPC_OK;
+}
+
+void lmpc_destroy(lmpc_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_bufs(c);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int lmpc_set_options(lmpc_ctx* c, const lmpc_options* o) {
+    if (!c || !o || o->max_iter < 1 || o->max_rounds < 1 || o->max_attempts < 1 || !(o->tol_mu > 0.0) ||
+        !(o->tol_p >= 0.0) || !(o->tol_d >= 0.0))
+        return LMPC_ERR_ARG;
+    fill_options(c->prm, o);
+    return LMPC_OK;
+}
+
+int lmpc_set_params(lmpc_ctx* c, const lmpc_params* p) {
+    if (!c || !params_ok(p)) return LMPC_ERR_ARG;
+    fill_params(c->prm, p);
+    return LMPC_OK;
+}
+
+int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, int batch, double* d_grf,
+                            int32_t* d_status, int32_t* d_iters, void* stream) {
+    if (!c || batch < 0 || (batch > 0 && (!d_rec || !d_contact || !d_grf))) return LMPC_ERR_ARG;
+    if (batch == 0) return LMPC_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const hipError_t e = lmpc::launch_qp(c->prm, d_rec, d_contact, batch, d_grf, d_status, d_iters, s);
+    if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
+    return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
+}
+
+int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int batch, double* grf,
+                     int32_t* status, int32_t* iters) {
+    if (!c || batch < 0 || batch > c->max_batch || (batch > 0 && (!rec || !contact || !grf))) return LMPC_ERR_ARG;
+    if (batch == 0) return LMPC_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
+    const size_t rl = (size_t)lmpc_record_len(c->H);
+    hipStream_t s = c->stream;
+    if (hipMemcpyAsync(c->d_rec, rec, (size_t)batch * rl * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(c->d_contact, contact, (size_t)batch * 4 * c->H, hipMemcpyHostToDevice, s) != hipSuccess)
+        return LMPC_ERR_DEVICE;
+    int rc = lmpc_solve_batch_device(c, c->d_rec, c->d_contact, batch, c->d_grf, c->d_status, c->d_iters, s);
+    if (rc != LMPC_OK) return rc;
+    if (hipMemcpyAsync(grf, c->d_grf, (size_t)batch * 12 * c->H * sizeof(double), hipMemcpyDeviceToHost, s) !=
+        hipSuccess)
+        return LMPC_ERR_DEVICE;
+    if (status && hipMemcpyAsync(status, c->d_status, (size_t)batch * sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
+                      hipSuccess)
+        return LMPC_ERR_DEVICE;
+    if (iters && hipMemcpyAsync(iters, c->d_iters, (size_t)batch * sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
+                     hipSuccess)
+        return LMPC_ERR_DEVICE;
+    return hipStreamSynchronize(s) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
+}
+
+int lmpc_sync(lmpc_ctx* c) {
+    if (!c) return LMPC_ERR_ARG;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
+}
+
+}  // extern "C"

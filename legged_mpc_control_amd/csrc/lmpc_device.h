@@ -1,0 +1,31 @@
+// lmpc_device.h -- device-side parameter block shared by the kernels and the C-ABI.
+#pragma once
+#include <cstdint>
+
+namespace lmpc {
+
+// Kernel argument block (by value).  All fp64, as in the reference (Eigen double).
+struct DevParams {
+    double q[12];      // state weights  (ConvexQPSolver.cpp:30)
+    double r[12];      // input weights  (ConvexQPSolver.cpp:31)
+    double mass;       // robot_mass     (ConvexQPSolver.cpp:280)
+    double Ib[9];      // body inertia, row-major
+    double mu;         // 0.3            (ConvexQPSolver.cpp:25)
+    double fmax;       // 180            (ConvexQPSolver.cpp:171)
+    double grav;       // 9.8            (ConvexQPSolver.cpp:175)
+    double dt;         // 0.01           (ConvexQPSolver.cpp:26)
+    double tol_mu;     // IPM stop: mean complementarity
+    double tol_p;      // polish primal tolerance (relative to fmax)
+    double tol_d;      // polish dual tolerance (relative to gradient scale)
+    int H;             // horizon
+    int max_iter;      // IPM iteration cap (per attempt)
+    int max_rounds;    // polish rounds per attempt
+    int max_attempts;  // IPM+polish attempts (tol_mu tightened x1e-3 per attempt)
+};
+
+// LDS footprint (doubles) of one QP for horizon H; must match the carve in lmpc_kernels.hip.
+inline int lds_doubles(int H) {
+    return 72 + 2 * H + 12 * H + 40 + 96 * H + 144 * H * 2 + 12 * H * 3 + 12 * (H + 1) + 144 * 3 + 16 + 64;
+}
+
+}  // namespace lmpc

@@ -1,0 +1,232 @@
+"""Host-side mirror of the reference's convex-MPC solver interface over the C-ABI.
+
+`ConvexQPSolver` keeps the reference's method names and call sequence
+(src/legged_ctrl/src/mpc_ctrl/convex_mpc/ConvexMpc.cpp:70-72):
+
+    solver = ConvexQPSolver(q_weights, r_weights)          # ConvexQPSolver.cpp:16
+    solver.calc_mpc_reference(state, leg_fsm)              # ConvexQPSolver.cpp:254-313
+    solver.update_cons_matrix()                            # ConvexQPSolver.cpp:230-239 (no-op)
+    grf = solver.compute_grfs(state)                       # ConvexQPSolver.cpp:314-327 -> (12,)
+
+`BatchedConvexQPSolver` is the batched form (host numpy or device torch
+buffers).  Both run the HIP kernel; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as N
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class BatchedConvexQPSolver:
+    """A device context: horizon H, host staging for up to max_batch QPs."""
+
+    def __init__(self, params: N.LmpcParams, horizon: int, max_batch: int = 1, device: int = 0,
+                 options: N.LmpcOptions | None = None):
+        if not (1 <= horizon <= N.LMPC_MAX_HORIZON):
+            raise ValueError(f"horizon must be in [1, {N.LMPC_MAX_HORIZON}]")
+        self._L = N.lib()
+        self.H = int(horizon)
+        self.max_batch = int(max_batch)
+        self.params = params
+        self._ctx = ctypes.c_void_p()
+        N.check(self._L.lmpc_create(ctypes.byref(params), self.H, self.max_batch, int(device),
+                                    ctypes.byref(self._ctx)), "lmpc_create")
+        if options is not None:
+            self.set_options(options)
+
+    @property
+    def record_len(self) -> int:
+        return 33 + 12 * self.H
+
+    def set_options(self, o: N.LmpcOptions) -> None:
+        N.check(self._L.lmpc_set_options(self._ctx, ctypes.byref(o)), "lmpc_set_options")
+
+    def set_params(self, p: N.LmpcParams) -> None:
+        N.check(self._L.lmpc_set_params(self._ctx, ctypes.byref(p)), "lmpc_set_params")
+        self.params = p
+
+    def solve(self, rec: np.ndarray, contact: np.ndarray):
+        """Host arrays in -> (grf [B,H,12], status [B], iters [B]); synchronous."""
+        rec = np.ascontiguousarray(rec, dtype=np.float64)
+        contact = np.ascontiguousarray(contact, dtype=np.uint8)
+        B = rec.shape[0]
+        if rec.shape != (B, self.record_len) or contact.shape != (B, self.H, 4):
+            raise ValueError("bad record/contact shape")
+        grf = np.zeros((B, self.H, 12), dtype=np.float64)
+        status = np.zeros(B, dtype=np.int32)
+        iters = np.zeros(B, dtype=np.int32)
+        N.check(self._L.lmpc_solve_batch(self._ctx, _dp(rec), contact.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                         B, _dp(grf), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                         iters.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "lmpc_solve_batch")
+        return grf, status, iters
+
+    def solve_device(self, rec, contact, grf, status=None, iters=None, stream=None) -> None:
+        """Device tensors (torch, resident in HBM) in/out; asynchronous on `stream`
+        (a torch.cuda.Stream or raw hipStream_t int; default = torch's current stream)."""
+        import torch
+
+        B = rec.shape[0]
+        for t, dt in ((rec, torch.float64), (contact, torch.uint8), (grf, torch.float64)):
+            if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+                raise ValueError("solve_device expects contiguous device tensors (f64 rec/grf, u8 contact)")
+        if rec.shape != (B, self.record_len) or contact.shape != (B, self.H, 4) or grf.shape != (B, self.H, 12):
+            raise ValueError("bad record/contact/grf shape")
+        if stream is None:
+            stream = torch.cuda.current_stream(rec.device)
+        sptr = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        N.check(self._L.lmpc_solve_batch_device(
+            self._ctx, rec.data_ptr(), contact.data_ptr(), B, grf.data_ptr(),
+            None if status is None else status.data_ptr(), None if iters is None else iters.data_ptr(),
+            sptr), "lmpc_solve_batch_device")
+
+    def close(self) -> None:
+        if self._ctx:
+            self._L.lmpc_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# Reference-shaped single-instance API
+# ---------------------------------------------------------------------------
+@dataclass
+class LeggedFeedback:
+    """Fields of LeggedFeedback read by the path (LeggedState.h:29-34,52)."""
+    root_euler: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_pos: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_ang_vel: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_lin_vel: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_rot_mat: np.ndarray = field(default_factory=lambda: np.eye(3))
+    foot_pos_abs: np.ndarray = field(default_factory=lambda: np.zeros((3, 4)))  # 3 x NUM_LEG
+
+
+@dataclass
+class LeggedCtrl:
+    """Fields of LeggedCtrl read/written by the path (LeggedState.h:79-96)."""
+    root_euler_d: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_pos_d: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_lin_vel_d_rel: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_lin_vel_d_world: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    root_ang_vel_d_rel: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    plan_contacts: np.ndarray = field(default_factory=lambda: np.ones(4, dtype=bool))
+
+
+@dataclass
+class LeggedParam:
+    q_weights: np.ndarray = field(default_factory=lambda: np.zeros(12))
+    r_weights: np.ndarray = field(default_factory=lambda: np.full(12, 1e-4))
+    robot_mass: float = 13.0
+    a1_trunk_inertia: np.ndarray = field(default_factory=lambda: np.diag([0.0158533, 0.0377999, 0.0456542]))
+    gait_counter_speed: float = 4.0
+
+
+@dataclass
+class LeggedState:
+    fbk: LeggedFeedback = field(default_factory=LeggedFeedback)
+    ctrl: LeggedCtrl = field(default_factory=LeggedCtrl)
+    param: LeggedParam = field(default_factory=LeggedParam)
+
+
+class LeggedContactFSM:
+    """Gait-phase part of LeggedContactFSM used by the QP (LeggedContactFSM.cpp:5-36,93-212,280-294).
+    Swing-trajectory generation (Bezier) is outside the QP path."""
+
+    def __init__(self):
+        self.leg_id = 0
+        self.gait = N.GAIT_TROT
+        self.gait_phase = 0.0
+        self.gait_speed = 4.0
+
+    def reset_params(self, state: LeggedState, leg_id: int) -> None:
+        self.leg_id = leg_id
+        self.gait_speed = float(state.param.gait_counter_speed)
+        self.set_default_gait_pattern()
+
+    def set_default_gait_pattern(self):
+        self.gait = N.GAIT_TROT
+
+    def set_crawl_gait_pattern(self):
+        self.gait = N.GAIT_CRAWL
+
+    def set_trot_with_stand_gait_pattern(self):
+        self.gait = N.GAIT_TROT_WITH_STAND
+
+    def set_default_stand_pattern(self):
+        self.gait = N.GAIT_STAND
+
+    def reset(self) -> None:
+        self.gait_phase = 0.0
+
+    def get_contact_state(self) -> int:
+        return N.lib().lmpc_current_contact(self.gait, self.leg_id, self.gait_phase)
+
+    def predict_contact_state(self, dt: float) -> int:
+        return N.lib().lmpc_predict_contact(self.gait, self.leg_id, self.gait_phase, self.gait_speed, dt)
+
+
+class ConvexQPSolver:
+    """Drop-in shaped like legged::ConvexQPSolver (ConvexQPSolver.h:23-40)."""
+
+    def __init__(self, q_weights, r_weights, horizon: int = 30, robot_mass: float = 13.0,
+                 trunk_inertia=None, mu: float = 0.3, f_max: float = 180.0, gravity: float = 9.8,
+                 dt: float = 0.01, device: int = 0):
+        p = N.LmpcParams()
+        for i in range(12):
+            p.q_weights[i] = float(q_weights[i])
+            p.r_weights[i] = float(r_weights[i])
+        p.robot_mass = float(robot_mass)
+        I = np.diag([0.0158533, 0.0377999, 0.0456542]) if trunk_inertia is None else np.asarray(trunk_inertia)
+        for i, v in enumerate(np.asarray(I, dtype=np.float64).reshape(9)):
+            p.trunk_inertia[i] = float(v)
+        p.mu, p.f_max, p.gravity, p.dt = float(mu), float(f_max), float(gravity), float(dt)
+        self.H = int(horizon)
+        self._p = p
+        self._dev = BatchedConvexQPSolver(p, self.H, 1, device)
+        self._rec = np.zeros((1, 33 + 12 * self.H))
+        self._con = np.ones((1, self.H, 4), dtype=np.uint8)
+        self.last_status = 0
+
+    def calc_mpc_reference(self, state: LeggedState, leg_FSM) -> None:
+        st = N.LmpcStateIn()
+        st.root_euler[:] = list(state.fbk.root_euler)
+        st.root_pos[:] = list(state.fbk.root_pos)
+        st.root_ang_vel[:] = list(state.fbk.root_ang_vel)
+        st.root_lin_vel[:] = list(state.fbk.root_lin_vel)
+        st.root_rot_mat[:] = list(np.asarray(state.fbk.root_rot_mat, dtype=np.float64).reshape(9))
+        st.foot_pos_abs[:] = list(np.asarray(state.fbk.foot_pos_abs, dtype=np.float64).T.reshape(12))
+        st.root_euler_d[:] = list(state.ctrl.root_euler_d)
+        st.root_pos_d[:] = list(state.ctrl.root_pos_d)
+        st.root_lin_vel_d_rel[:] = list(state.ctrl.root_lin_vel_d_rel)
+        st.root_ang_vel_d_rel[:] = list(state.ctrl.root_ang_vel_d_rel)
+        vdw = np.zeros(3)
+        N.check(N.lib().lmpc_pack_record(ctypes.byref(self._p), self.H, ctypes.byref(st), _dp(self._rec[0]),
+                                         _dp(vdw)), "lmpc_pack_record")
+        state.ctrl.root_lin_vel_d_world = vdw  # ConvexQPSolver.cpp:260 writes it back
+        # update_bound_constraints (ConvexQPSolver.cpp:329-346)
+        for j in range(4):
+            self._con[0, 0, j] = 1 if state.ctrl.plan_contacts[j] else 0
+        for i in range(1, self.H):
+            for j in range(4):
+                self._con[0, i, j] = leg_FSM[j].predict_contact_state(i * self._p.dt)
+
+    def update_cons_matrix(self) -> None:
+        """No-op: the constraint values are built on the device inside the solve."""
+
+    def compute_grfs(self, state: LeggedState) -> np.ndarray:
+        grf, status, _ = self._dev.solve(self._rec, self._con)
+        self.last_status = int(status[0])
+        self.last_solution = grf[0]
+        return grf[0, 0].copy()  # u_0: FL, FR, RL, RR x (fx, fy, fz), world frame

@@ -1,0 +1,73 @@
+"""Robot presets and seeded synthetic problem batches (host side, via the C-ABI).
+
+Instances are keyed by (seed, global_index) with a counter-based Philox4x32-10
+generator, so every rank (and the CPU oracle) builds identical inputs without
+moving any bytes.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+# BASELINE.json configs -> (robot, gait, H, batch)
+CONFIGS = {
+    1: dict(name="a1_standing_h10", robot="a1", gait=N.GAIT_TROT, H=10, batch=1, standing=True),
+    2: dict(name="go1_trot_h10_b1024", robot="go1", gait=N.GAIT_TROT, H=10, batch=1024, standing=False),
+    3: dict(name="go1_trot_h20_b8192", robot="go1", gait=N.GAIT_TROT, H=20, batch=8192, standing=False),
+    4: dict(name="go1_mixed_h10_b65536", robot="go1", gait=-1, H=10, batch=65536, standing=False),
+    5: dict(name="go1_trot_h30_b4096", robot="go1", gait=N.GAIT_TROT, H=30, batch=4096, standing=False),
+}
+BASE_SEED = 20261015
+
+
+def params(robot: str = "go1") -> N.LmpcParams:
+    p = N.LmpcParams()
+    if robot == "go1":
+        N.lib().lmpc_params_go1(ctypes.byref(p))
+    elif robot == "a1":
+        N.lib().lmpc_params_a1(ctypes.byref(p))
+    else:
+        raise ValueError(robot)
+    return p
+
+
+def synth_cfg(robot: str = "go1", gait: int = N.GAIT_TROT, standing: bool = False) -> N.LmpcSynthCfg:
+    c = N.LmpcSynthCfg()
+    if standing:
+        N.lib().lmpc_synth_cfg_a1_standing(ctypes.byref(c))
+    else:
+        N.lib().lmpc_synth_cfg_go1(ctypes.byref(c))
+        if robot == "a1":
+            # A1 sim: feet (+-0.17, +-0.17, -0.3), gait speed 3.5 (gazebo_a1_convex.yaml:19-36)
+            a1 = N.LmpcSynthCfg()
+            N.lib().lmpc_synth_cfg_a1_standing(ctypes.byref(a1))
+            c.default_feet[:] = a1.default_feet[:]
+            c.gait_speed = a1.gait_speed
+        c.gait = gait
+    return c
+
+
+def fill(p: N.LmpcParams, cfg: N.LmpcSynthCfg, H: int, count: int, seed: int, first_index: int = 0):
+    """-> (rec [count, 33+12H] f64, contact [count, H, 4] u8)."""
+    rl = 33 + 12 * H
+    rec = np.zeros((count, rl), dtype=np.float64)
+    con = np.zeros((count, H, 4), dtype=np.uint8)
+    rc = N.lib().lmpc_synth_fill(ctypes.byref(p), ctypes.byref(cfg), H, seed, first_index, count,
+                                 rec.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                 con.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    N.check(rc, "lmpc_synth_fill")
+    return rec, con
+
+
+def config_batch(config_id: int, count: int | None = None, first_index: int = 0, H: int | None = None):
+    """Synthetic batch for a BASELINE.json config -> (params, H, rec, contact)."""
+    c = CONFIGS[config_id]
+    H = c["H"] if H is None else H
+    p = params(c["robot"])
+    cfg = synth_cfg(c["robot"], c["gait"], c["standing"])
+    n = c["batch"] if count is None else count
+    rec, con = fill(p, cfg, H, n, BASE_SEED + config_id, first_index)
+    return p, H, rec, con

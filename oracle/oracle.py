@@ -1,0 +1,162 @@
+"""ctypes wrapper of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker.  The oracle restates the reference's
+ConvexQPSolver QP (src/legged_ctrl/src/mpc_ctrl/convex_mpc/ConvexQPSolver.cpp:
+16-346) and solves it exactly (dense Goldfarb-Idnani); see lmpc_oracle.h.
+Parity unpinned: the reference has no fixtures for this path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liblmpc_oracle.so")
+_lock = threading.Lock()
+_lib = None
+
+
+class OracleParams(ctypes.Structure):
+    _fields_ = [
+        ("q_weights", ctypes.c_double * 12),
+        ("r_weights", ctypes.c_double * 12),
+        ("robot_mass", ctypes.c_double),
+        ("trunk_inertia", ctypes.c_double * 9),
+        ("mu", ctypes.c_double),
+        ("f_max", ctypes.c_double),
+        ("gravity", ctypes.c_double),
+        ("dt", ctypes.c_double),
+    ]
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with gcc (make) into oracle/build/."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            build()
+            L = ctypes.CDLL(_LIB_PATH)
+            dp = ctypes.POINTER(ctypes.c_double)
+            u8p = ctypes.POINTER(ctypes.c_uint8)
+            i32p = ctypes.POINTER(ctypes.c_int32)
+            ip = ctypes.POINTER(ctypes.c_int)
+            pp = ctypes.POINTER(OracleParams)
+            L.oracle_build_sparse_qp.argtypes = [pp, ctypes.c_int, dp, u8p, dp, dp, dp, dp, dp]
+            L.oracle_build_sparse_qp.restype = None
+            L.oracle_update_A.argtypes = [ctypes.c_double, ctypes.c_double, dp]
+            L.oracle_update_B.argtypes = [pp, dp, dp, dp]
+            L.oracle_condense.argtypes = [ctypes.c_int, dp, dp, dp, dp, dp, dp, dp, dp]
+            L.oracle_condense.restype = ctypes.c_int
+            L.oracle_solve.argtypes = [pp, ctypes.c_int, dp, u8p, dp, dp, ip]
+            L.oracle_solve.restype = ctypes.c_int
+            L.oracle_solve_batch.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, u8p, dp, i32p, ctypes.c_int]
+            L.oracle_solve_batch.restype = ctypes.c_int
+            L.oracle_gi_solve.argtypes = [ctypes.c_int, dp, dp, ctypes.c_int, dp, dp, dp, dp, ip]
+            L.oracle_gi_solve.restype = ctypes.c_int
+            L.oracle_predict_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double]
+            L.oracle_predict_contact.restype = ctypes.c_int
+            L.oracle_current_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
+            L.oracle_current_contact.restype = ctypes.c_int
+            _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _u8p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def make_params(q_weights, r_weights, robot_mass=13.0, trunk_inertia=None, mu=0.3, f_max=180.0,
+                gravity=9.8, dt=0.01) -> OracleParams:
+    p = OracleParams()
+    for i in range(12):
+        p.q_weights[i] = float(q_weights[i])
+        p.r_weights[i] = float(r_weights[i])
+    p.robot_mass = float(robot_mass)
+    I = np.diag([0.0158533, 0.0377999, 0.0456542]) if trunk_inertia is None else np.asarray(trunk_inertia)
+    for i, v in enumerate(np.asarray(I, dtype=np.float64).reshape(9)):
+        p.trunk_inertia[i] = float(v)
+    p.mu, p.f_max, p.gravity, p.dt = float(mu), float(f_max), float(gravity), float(dt)
+    return p
+
+
+def params_from(struct) -> OracleParams:
+    """Copy any ctypes struct with the lmpc_params field layout."""
+    p = OracleParams()
+    ctypes.memmove(ctypes.byref(p), ctypes.byref(struct), ctypes.sizeof(OracleParams))
+    return p
+
+
+def build_sparse_qp(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray):
+    n, m = 24 * H, 32 * H
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    P = np.zeros(n); q = np.zeros(n); A = np.zeros((m, n)); l = np.zeros(m); u = np.zeros(m)
+    lib().oracle_build_sparse_qp(ctypes.byref(p), H, _dp(rec), _u8p(contact), _dp(P), _dp(q), _dp(A), _dp(l), _dp(u))
+    return P, q, A, l, u
+
+
+def condense(H: int, P, q, A, l):
+    N = 12 * H
+    Hc = np.zeros((N, N)); g = np.zeros(N); T = np.zeros((12 * H, N)); c = np.zeros(12 * H)
+    rc = lib().oracle_condense(H, _dp(np.ascontiguousarray(P)), _dp(np.ascontiguousarray(q)),
+                               _dp(np.ascontiguousarray(A)), _dp(np.ascontiguousarray(l)),
+                               _dp(Hc), _dp(g), _dp(T), _dp(c))
+    if rc != 0:
+        raise RuntimeError(f"oracle_condense failed: {rc}")
+    return Hc, g, T, c
+
+
+def solve(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray):
+    """Exact optimum of one instance -> (grf[H,12], kkt[4], n_active)."""
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    grf = np.zeros(12 * H); kkt = np.zeros(4); na = ctypes.c_int(0)
+    rc = lib().oracle_solve(ctypes.byref(p), H, _dp(rec), _u8p(contact), _dp(grf), _dp(kkt), ctypes.byref(na))
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve failed: {rc}")
+    return grf.reshape(H, 12), kkt, na.value
+
+
+def solve_batch(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray, n_threads: int = 1):
+    B = rec.shape[0]
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    grf = np.zeros((B, H, 12)); status = np.zeros(B, dtype=np.int32)
+    fails = lib().oracle_solve_batch(ctypes.byref(p), H, B, _dp(rec), _u8p(contact), _dp(grf),
+                                     status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n_threads)
+    return grf, status, fails
+
+
+def gi_solve(G, g0, CI, ci0):
+    """min 1/2 x'Gx + g0'x  s.t. CI x + ci0 >= 0 (CI rows = constraints)."""
+    G = np.ascontiguousarray(G, dtype=np.float64)
+    n = G.shape[0]
+    CI = np.ascontiguousarray(CI, dtype=np.float64)
+    m = CI.shape[0]
+    x = np.zeros(n); lam = np.zeros(max(m, 1)); na = ctypes.c_int(0)
+    rc = lib().oracle_gi_solve(n, _dp(G), _dp(np.ascontiguousarray(g0, dtype=np.float64)), m, _dp(CI),
+                               _dp(np.ascontiguousarray(ci0, dtype=np.float64)), _dp(x), _dp(lam), ctypes.byref(na))
+    return rc, x, lam[:m], na.value
+
+
+def predict_contact(gait: int, leg: int, phase: float, speed: float, dt: float) -> int:
+    return lib().oracle_predict_contact(gait, leg, phase, speed, dt)
+
+
+def current_contact(gait: int, leg: int, phase: float) -> int:
+    return lib().oracle_current_contact(gait, leg, phase)
