@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: batched convex-MPC GRF QP solves/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--batch B]
+
+One step = one fused-kernel pass over one batch of synthetic QPs already
+resident in HBM (config 2 by default: Go1 trot, horizon 10, 1024 QPs per GPU).
+For N > 1 (launched by torch.distributed.run, one rank per GPU) each rank
+builds and solves its own shard of global indices [rank*B, (rank+1)*B): no
+data-path collective (independent QPs, weak scaling).  Rank 0 prints ONE JSON
+line with the roofline of the dominant kernel (HIP events on the launch stream)
+and, at N=1, the CPU oracle timed on the host cores over the same instances
+together with the max GRF error against it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, help="BASELINE.json config id (2,3,4,5)")
+    ap.add_argument("--batch", type=int, default=None, help="QPs per GPU (default: config batch; config 4: 65536/N)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall seconds)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    from legged_mpc_control_amd import BatchedConvexQPSolver, roofline, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = synth.CONFIGS[args.config]
+    H = cfg["H"]
+    if args.batch is not None:
+        B = args.batch
+    elif args.config == 4:
+        B = cfg["batch"] // world
+    else:
+        B = cfg["batch"]
+    first = rank * B
+    p, H, rec, con = synth.config_batch(args.config, count=B, first_index=first)
+
+    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank)
+    d_rec = torch.from_numpy(rec).to(dev)
+    d_con = torch.from_numpy(con).to(dev)
+    d_grf = torch.empty((B, H, 12), dtype=torch.float64, device=dev)
+    d_st = torch.empty(B, dtype=torch.int32, device=dev)
+    d_it = torch.empty(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(dev)  # dedicated launch stream: events below bracket exactly the kernels
+    torch.cuda.set_stream(stream)
+
+    for _ in range(args.warmup):
+        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream)
+    torch.cuda.synchronize(dev)
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_max = elapsed
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    grf = d_grf.cpu().numpy()
+    st = d_st.cpu().numpy()
+    it = d_it.cpu().numpy()
+    ipm_mean = float(np.mean(it & 0xFFFF))
+    pol_mean = float(np.mean(it >> 16))
+    flop_per_qp = roofline.qp_flop(H, ipm_mean, pol_mean)
+    achieved_tf = flop_per_qp * B / (kernel_ms * 1e-3) / 1e12
+    total_qps = world * B * args.steps / t_max
+
+    stats = torch.tensor([float((st == 0).sum()), float((st == 1).sum()), float((st == 2).sum())],
+                         dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(stats)
+
+    cpu = None
+    max_err = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+
+        op = O.params_from(p)
+        cores = min(16, os.cpu_count() or 1)
+        ref, ost, _ = O.solve_batch(op, H, rec, con, n_threads=cores)  # warm + parity reference
+        max_err = float(np.max(np.abs(grf - ref) / np.maximum(1.0, np.abs(ref))))
+        reps = 0
+        t1 = time.perf_counter()
+        while True:
+            O.solve_batch(op, H, rec, con, n_threads=cores)
+            reps += 1
+            if time.perf_counter() - t1 >= args.cpu_seconds:
+                break
+        ct = time.perf_counter() - t1
+        cpu = {
+            "value": reps * B / ct,
+            "unit": "QP/s",
+            "cores": cores,
+            "kind": "port",
+            "sample": f"{reps} x the rank-0 batch ({B} QPs, {cfg['name']}), fp64 dense Goldfarb-Idnani "
+                      f"oracle over {cores} host threads, {ct:.1f} s wall",
+        }
+
+    if rank == 0:
+        line = {
+            "metric": "QP solves/sec (Go1, horizon=10, 12 contacts); max GRF err vs exact-QP oracle",
+            "value": total_qps,
+            "unit": "QP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Philox-seeded perturbed states, SURVEY.md 8d)",
+            "config": {
+                "workload": cfg["name"] if args.batch is None else f"{cfg['name']}@b{B}",
+                "horizon": H,
+                "batch_per_gpu": B,
+                "global_batch": B * world,
+                "robot": cfg["robot"],
+                "gait": "mixed" if cfg["gait"] < 0 else ["trot", "crawl", "trot_with_stand", "stand"][cfg["gait"]],
+                "parallelism": f"dp{world} (independent QP shards, no collective)",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "achieved": achieved_tf,
+                "peak": roofline.FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved_tf / roofline.FP64_PEAK_TFLOPS,
+                "traffic": None,
+                "kernel": "lmpc_qp_kernel",
+                "kernel_ms": kernel_ms,
+                "flop_per_qp": flop_per_qp,
+                "hbm_gbs": roofline.qp_bytes(H) * B / (kernel_ms * 1e-3) / 1e9,
+            },
+            "cpu_baseline": cpu,
+            "max_grf_err": max_err,
+            "qp_status": {"converged": int(stats[0]), "max_iter": int(stats[1]), "nan": int(stats[2])},
+            "ipm_iters_mean": ipm_mean,
+            "polish_rounds_mean": pol_mean,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

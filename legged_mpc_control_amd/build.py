@@ -1,0 +1,64 @@
+"""In-tree build of the HIP library (hipcc, gfx950 only) and the C++ host mirror test."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIBDIR, "liblmpc.so")
+ARCH = "gfx950"
+
+SOURCES = ["lmpc_kernels.hip", "lmpc_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
+HEADERS = ["lmpc_device.h"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [
+        os.path.join(ROOT, "include", "lmpc", "lmpc.h"), os.path.join(ROOT, "include", "lmpc", "ConvexQPSolver.hpp")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_cpp_test(force: bool = False) -> str:
+    """C++ program that drives legged::ConvexQPSolver exactly like ConvexMpc::grf_update."""
+    src = os.path.join(ROOT, "tests", "cpp", "grf_update_test.cpp")
+    out = os.path.join(ROOT, "tests", "cpp", "build", "grf_update_test")
+    if not force and not _stale(out, [src, LIB]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", out, src,
+           "-L", LIBDIR, "-llmpc", f"-Wl,-rpath,{LIBDIR}"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+if __name__ == "__main__":
+    print(build_native(force=True, verbose=True))

@@ -63,11 +63,11 @@ bool params_ok(const lmpc_params* p) {
 }
 
 void free_bufs(lmpc_ctx* c) {
-    hipFree(c->d_rec);
-    hipFree(c->d_contact);
-    hipFree(c->d_grf);
-    hipFree(c->d_status);
-    hipFree(c->d_iters);
+    (void)hipFree(c->d_rec);
+    (void)hipFree(c->d_contact);
+    (void)hipFree(c->d_grf);
+    (void)hipFree(c->d_status);
+    (void)hipFree(c->d_iters);
     c->d_rec = nullptr;
     c->d_contact = nullptr;
     c->d_grf = nullptr;
@@ -108,7 +108,7 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
                   hipMalloc(&c->d_iters, (size_t)max_batch * sizeof(int32_t)) == hipSuccess;
         if (!ok) {
             free_bufs(c);
-            hipStreamDestroy(c->stream);
+            (void)hipStreamDestroy(c->stream);
             delete c;
             return LMPC_ERR_ALLOC;
         }
@@ -119,10 +119,10 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
 
 void lmpc_destroy(lmpc_ctx* c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_bufs(c);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 

@@ -1,0 +1,43 @@
+"""Algorithmic work model of the fused QP kernel (used by bench.py's roofline).
+
+Counts are the useful fp64 flops of the algorithm (FMA = 2 flops), per horizon
+stage, derived from lmpc_kernels.hip (DESIGN.md "Roofline" explains each term):
+
+  Riccati factorisation stage (riccati_factor):
+    Bt = G0 T (216 FMA) + G0 up (72) + PB = P[:,6:12] Bt (864) + v = P d (72)
+    + Guu = T'RtT + Bt'PB[6:12] (324 + 864) + Gux = PB'A (180)
+    + Cholesky(12) + L^-1 Gux + L^-1 (288 + 864 + 288)
+    + P(I+dtN), (I+dtN')PA (500) + Y'Y symmetric (936)            = 5468 FMA
+  Riccati vector pass stage (riccati_solve): backward 450 FMA + forward 410 = 860 FMA
+  Adjoint stage (adjoint_grad): 120 FMA
+  IPM iteration  = 1 factorisation + 2 vector passes (predictor + corrector)
+  polish round   = 1 factorisation + 1 vector pass + 1 adjoint
+"""
+from __future__ import annotations
+
+FACT_FLOP_PER_STAGE = 2 * 5468
+SOLVE_FLOP_PER_STAGE = 2 * 860
+ADJ_FLOP_PER_STAGE = 2 * 120
+LEG_FLOP_PER_IPM_ITER = 2 * 60      # per stance leg-step: W, C'WC, C'w, step lengths
+LEG_FLOP_PER_POLISH = 2 * 80        # per stance leg-step: null basis + verification
+
+FP64_PEAK_TFLOPS = 78.6             # MI355X FP64 (vector = matrix), SURVEY.md 8d / AMD spec
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
+
+
+def ipm_iter_flop(H: int) -> int:
+    return H * (FACT_FLOP_PER_STAGE + 2 * SOLVE_FLOP_PER_STAGE) + 4 * H * LEG_FLOP_PER_IPM_ITER
+
+
+def polish_round_flop(H: int) -> int:
+    return H * (FACT_FLOP_PER_STAGE + SOLVE_FLOP_PER_STAGE + ADJ_FLOP_PER_STAGE) + 4 * H * LEG_FLOP_PER_POLISH
+
+
+def qp_flop(H: int, ipm_iters: float, polish_rounds: float) -> float:
+    """Algorithmic flops of one QP given its (mean) IPM iterations and polish rounds."""
+    return ipm_iters * ipm_iter_flop(H) + polish_rounds * polish_round_flop(H)
+
+
+def qp_bytes(H: int) -> int:
+    """HBM bytes per QP: record (33+12H doubles) + contact (4H) + GRF out (12H doubles) + status + iters."""
+    return (33 + 12 * H) * 8 + 4 * H + 12 * H * 8 + 8
