@@ -110,6 +110,10 @@ void lmpc_destroy(lmpc_ctx* ctx);
 int lmpc_set_options(lmpc_ctx* ctx, const lmpc_options* o);
 int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
 
+/* Pre-allocates the per-QP factor workspace for batches up to `batch` (the
+ * device path grows it on demand; call this before capturing a HIP graph). */
+int lmpc_reserve(lmpc_ctx* ctx, int batch);
+
 /* Host buffers in/out, synchronous.  rec[batch][33+12H], contact[batch][H][4],
  * grf[batch][H][12]; status[batch] and iters[batch] may be NULL. */
 int lmpc_solve_batch(lmpc_ctx* ctx, const double* rec, const uint8_t* contact, int batch,

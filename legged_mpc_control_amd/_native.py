@@ -23,7 +23,7 @@ GAIT_TROT, GAIT_CRAWL, GAIT_TROT_WITH_STAND, GAIT_STAND = 0, 1, 2, 3
 EXPORTED_SYMBOLS = (
     "lmpc_params_go1", "lmpc_params_a1", "lmpc_options_default", "lmpc_record_len",
     "lmpc_abi_version", "lmpc_strerror", "lmpc_create", "lmpc_destroy", "lmpc_set_options",
-    "lmpc_set_params", "lmpc_solve_batch", "lmpc_solve_batch_device", "lmpc_sync",
+    "lmpc_set_params", "lmpc_reserve", "lmpc_solve_batch", "lmpc_solve_batch_device", "lmpc_sync",
     "lmpc_predict_contact", "lmpc_current_contact", "lmpc_contact_schedule", "lmpc_pack_record",
     "lmpc_synth_cfg_go1", "lmpc_synth_cfg_a1_standing", "lmpc_synth_fill",
 )
@@ -114,6 +114,8 @@ def lib():
         L.lmpc_set_options.restype = ctypes.c_int
         L.lmpc_set_params.argtypes = [vp, pp]
         L.lmpc_set_params.restype = ctypes.c_int
+        L.lmpc_reserve.argtypes = [vp, ctypes.c_int]
+        L.lmpc_reserve.restype = ctypes.c_int
         L.lmpc_solve_batch.argtypes = [vp, dp, u8p, ctypes.c_int, dp, i32p, i32p]
         L.lmpc_solve_batch.restype = ctypes.c_int
         L.lmpc_solve_batch_device.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]

@@ -14,7 +14,7 @@
 
 namespace lmpc {
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, int batch, double* grf,
-                     int32_t* status, int32_t* iters, hipStream_t stream);
+                     int32_t* status, int32_t* iters, double* scratch, hipStream_t stream);
 }
 
 struct lmpc_ctx {
@@ -28,6 +28,8 @@ struct lmpc_ctx {
     double* d_grf = nullptr;
     int32_t* d_status = nullptr;
     int32_t* d_iters = nullptr;
+    double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
+    size_t scratch_qps = 0;
 };
 
 namespace {
@@ -68,6 +70,9 @@ void free_bufs(lmpc_ctx* c) {
     (void)hipFree(c->d_grf);
     (void)hipFree(c->d_status);
     (void)hipFree(c->d_iters);
+    (void)hipFree(c->d_scratch);
+    c->d_scratch = nullptr;
+    c->scratch_qps = 0;
     c->d_rec = nullptr;
     c->d_contact = nullptr;
     c->d_grf = nullptr;
@@ -113,6 +118,12 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
             return LMPC_ERR_ALLOC;
         }
     }
+    if (max_batch > 0 && lmpc_reserve(c, max_batch) != LMPC_OK) {
+        free_bufs(c);
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return LMPC_ERR_ALLOC;
+    }
     *out = c;
     return LMPC_OK;
 }
@@ -140,12 +151,35 @@ int lmpc_set_params(lmpc_ctx* c, const lmpc_params* p) {
     return LMPC_OK;
 }
 
+int lmpc_reserve(lmpc_ctx* c, int batch) {
+    if (!c || batch < 0) return LMPC_ERR_ARG;
+    if ((size_t)batch <= c->scratch_qps) return LMPC_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
+    if (c->d_scratch) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(c->d_scratch);
+        c->d_scratch = nullptr;
+        c->scratch_qps = 0;
+    }
+    if (hipMalloc(&c->d_scratch, (size_t)batch * lmpc::scratch_doubles_per_qp(c->H) * sizeof(double)) != hipSuccess) {
+        c->d_scratch = nullptr;
+        return LMPC_ERR_ALLOC;
+    }
+    c->scratch_qps = (size_t)batch;
+    return LMPC_OK;
+}
+
 int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, int batch, double* d_grf,
                             int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_rec || !d_contact || !d_grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    const hipError_t e = lmpc::launch_qp(c->prm, d_rec, d_contact, batch, d_grf, d_status, d_iters, s);
+    if ((size_t)batch > c->scratch_qps) {
+        const int rc = lmpc_reserve(c, batch);
+        if (rc != LMPC_OK) return rc;
+    }
+    const hipError_t e = lmpc::launch_qp(c->prm, d_rec, d_contact, batch, d_grf, d_status, d_iters, c->d_scratch, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
 }

@@ -1,5 +1,6 @@
 // lmpc_device.h -- device-side parameter block shared by the kernels and the C-ABI.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 namespace lmpc {
@@ -23,9 +24,10 @@ struct DevParams {
     int max_attempts;  // IPM+polish attempts (tol_mu tightened x1e-3 per attempt)
 };
 
-// LDS footprint (doubles) of one QP for horizon H; must match the carve in lmpc_kernels.hip.
-inline int lds_doubles(int H) {
-    return 72 + 2 * H + 12 * H + 40 + 96 * H + 144 * H * 2 + 12 * H * 3 + 12 * (H + 1) + 144 * 3 + 16 + 64;
-}
+// LDS footprint (doubles) of one QP for horizon H; must match carve() in lmpc_kernels.hip.
+inline int lds_doubles(int H) { return 1058 + 14 * H + 276 * H; }
+inline size_t lds_bytes(int H) { return (size_t)lds_doubles(H) * sizeof(double); }
+// Global scratch (doubles) per QP: L^-1, V, K, P2 per stage (GS = 243).
+inline size_t scratch_doubles_per_qp(int H) { return (size_t)243 * H; }
 
 }  // namespace lmpc
