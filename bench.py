@@ -43,10 +43,9 @@ def main():
     import torch
 
     from legged_mpc_control_amd import BatchedConvexQPSolver, roofline, synth
+    from legged_mpc_control_amd import dist as D
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local_rank = D.env_rank()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
@@ -65,7 +64,7 @@ def main():
         B = cfg["batch"] // world
     else:
         B = cfg["batch"]
-    first = rank * B
+    first, _ = D.shard_range(rank, world, B)
     p, H, rec, con = synth.config_batch(args.config, count=B, first_index=first)
 
     solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank)
@@ -94,11 +93,7 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t_max = elapsed
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
+    t_max = D.max_over_ranks(elapsed, dist, dev)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
     grf = d_grf.cpu().numpy()
@@ -110,10 +105,7 @@ def main():
     achieved_tf = flop_per_qp * B / (kernel_ms * 1e-3) / 1e12
     total_qps = world * B * args.steps / t_max
 
-    stats = torch.tensor([float((st == 0).sum()), float((st == 1).sum()), float((st == 2).sum())],
-                         dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(stats)
+    stats = D.sum_over_ranks([(st == 0).sum(), (st == 1).sum(), (st == 2).sum()], dist, dev)
 
     cpu = None
     max_err = None

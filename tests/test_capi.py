@@ -1,0 +1,97 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every
+symbol include/lmpc/lmpc.h declares, and rejects bad arguments without a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+from legged_mpc_control_amd import _native as N
+
+HEADER = os.path.join(ROOT, "include", "lmpc", "lmpc.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lmpc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declarations_are_all_exported():
+    lib = N.lib()
+    decl = declared_functions()
+    assert len(decl) >= 20
+    for name in decl:
+        assert hasattr(lib, name), f"{name} declared in lmpc.h but not exported"
+    assert sorted(N.EXPORTED_SYMBOLS) == decl
+
+
+def test_exports_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    syms = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    for name in declared_functions():
+        assert name in syms  # unmangled
+
+
+def test_abi_and_strings():
+    lib = N.lib()
+    assert lib.lmpc_abi_version() == 1
+    assert lib.lmpc_record_len(10) == 153 and lib.lmpc_record_len(30) == 393
+    assert lib.lmpc_strerror(0) == b"ok"
+    assert lib.lmpc_strerror(-1) == b"invalid argument"
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(N.LmpcParams) == 8 * (12 + 12 + 1 + 9 + 4)
+    assert ctypes.sizeof(N.LmpcOptions) == 4 * 3 + 4 + 8 * 3  # 3 ints + pad + 3 doubles
+    assert ctypes.sizeof(N.LmpcStateIn) == 8 * (3 * 4 + 9 + 12 + 3 * 4)
+
+
+def test_create_rejects_bad_arguments():
+    lib = N.lib()
+    p = N.LmpcParams()
+    lib.lmpc_params_go1(ctypes.byref(p))
+    ctx = ctypes.c_void_p()
+    assert lib.lmpc_create(ctypes.byref(p), 0, 1, 0, ctypes.byref(ctx)) == -1  # horizon 0
+    assert lib.lmpc_create(ctypes.byref(p), 33, 1, 0, ctypes.byref(ctx)) == -1  # > LMPC_MAX_HORIZON
+    bad = N.LmpcParams()
+    lib.lmpc_params_go1(ctypes.byref(bad))
+    bad.r_weights[0] = 0.0  # R must be positive definite (strict convexity)
+    assert lib.lmpc_create(ctypes.byref(bad), 10, 1, 0, ctypes.byref(ctx)) == -1
+    assert lib.lmpc_solve_batch(None, None, None, 1, None, None, None) == -1
+    assert lib.lmpc_solve_batch_device(None, None, None, 1, None, None, None, None) == -1
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    lib = N.lib()
+    p = N.LmpcParams()
+    lib.lmpc_params_go1(ctypes.byref(p))
+    ctx = ctypes.c_void_p()
+    assert lib.lmpc_create(ctypes.byref(p), 10, 4, 0, ctypes.byref(ctx)) == -2  # LMPC_ERR_DEVICE
+    assert not ctx.value
+
+
+def test_cpp_dropin_program_builds():
+    from legged_mpc_control_amd import build as B
+
+    exe = B.build_cpp_test()
+    assert os.path.exists(exe) and os.access(exe, os.X_OK)
+
+
+def test_no_oracle_in_product_path():
+    """The product package must never import or link the oracle (the checker)."""
+    pkg = os.path.join(ROOT, "legged_mpc_control_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", ".hpp")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle|lmpc_oracle|liblmpc_oracle", txt, re.M), f
+    out = subprocess.run(["ldd", N.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out

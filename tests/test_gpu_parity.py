@@ -1,0 +1,253 @@
+"""GPU parity tests (MI355X): the HIP path, called through the C-ABI, against the
+CPU oracle (exact optimum of the reference's QP) on the committed golden
+fixtures, on live seeded samples of every BASELINE config, and -- at the full
+batch sizes -- through size-independent properties (feasibility, determinism,
+permutation and shard invariance, device == host path).
+
+Tolerance (BASELINE.json north star): max over all H x 12 forces of
+|f_gpu - f_ref| / max(1, |f_ref|) <= 1e-4.  A tighter 1e-7 regression guard is
+also asserted (the kernel reaches ~1e-9: both solve the same QP exactly).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden_files, lmpc_params_from, load_golden, rel_err
+
+from legged_mpc_control_amd import BatchedConvexQPSolver, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4          # north-star parity bar
+TOL_REGRESS = 1e-7  # regression guard
+
+
+def feasibility_violation(grf, con, mu=0.3, fmax=180.0):
+    f = grf.reshape(grf.shape[0], -1, 4, 3)
+    c = con.astype(bool)
+    fx, fy, fz = f[..., 0], f[..., 1], f[..., 2]
+    v = np.maximum.reduce([np.abs(fx) - mu * fz, np.abs(fy) - mu * fz, -fz, fz - fmax * c])
+    swing_nonzero = np.any(f[~c] != 0.0)
+    return float(np.max(v)), bool(swing_nonzero)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: os.path.basename(p))
+def test_golden_fixtures(path):
+    g = load_golden(path)
+    s = BatchedConvexQPSolver(lmpc_params_from(g["params"]), g["H"], max_batch=g["rec"].shape[0])
+    grf, status, iters = s.solve(g["rec"], g["contact"])
+    assert np.all(status == 0), status
+    err = rel_err(grf, g["grf"])
+    assert err <= TOL
+    assert err <= TOL_REGRESS, f"regression: {err:.2e}"
+
+
+@pytest.mark.parametrize("cid,count,first", [(2, 256, 5000), (3, 48, 777), (4, 512, 12345), (5, 24, 99)])
+def test_live_samples_vs_oracle(cid, count, first):
+    p, H, rec, con = synth.config_batch(cid, count=count, first_index=first)
+    s = BatchedConvexQPSolver(p, H, max_batch=count)
+    grf, status, iters = s.solve(rec, con)
+    ref, ost, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
+    assert fails == 0
+    assert np.all(status == 0)
+    err = rel_err(grf, ref)
+    assert err <= TOL and err <= TOL_REGRESS, err
+
+
+def test_full_config2_batch_vs_oracle():
+    """Config 2 at its full size (1024 QPs): every QP against the oracle."""
+    p, H, rec, con = synth.config_batch(2)
+    s = BatchedConvexQPSolver(p, H, max_batch=rec.shape[0])
+    grf, status, iters = s.solve(rec, con)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
+    assert fails == 0 and np.all(status == 0)
+    assert rel_err(grf, ref) <= TOL_REGRESS
+
+
+@pytest.mark.parametrize("cid", [3, 4, 5])
+def test_full_size_properties(cid, torch_dev):
+    """Configs 3/4/5 at full batch: converged, feasible, swing legs exactly zero,
+    bitwise deterministic, permutation-invariant and shard-invariant."""
+    import torch
+
+    p, H, rec, con = synth.config_batch(cid)
+    B = rec.shape[0]
+    s = BatchedConvexQPSolver(p, H, max_batch=0)
+    d_rec, d_con = torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev)
+    out = torch.empty((B, H, 12), dtype=torch.float64, device=torch_dev)
+    st = torch.empty(B, dtype=torch.int32, device=torch_dev)
+    s.solve_device(d_rec, d_con, out, st)
+    torch.cuda.synchronize()
+    grf, status = out.cpu().numpy(), st.cpu().numpy()
+    assert np.all(status == 0), np.bincount(status)
+    viol, swing_nonzero = feasibility_violation(grf, con, p.mu, p.f_max)
+    assert viol <= 1e-9 * p.f_max and not swing_nonzero
+    # determinism
+    out2 = torch.empty_like(out)
+    s.solve_device(d_rec, d_con, out2, st)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    # permutation invariance
+    perm = torch.randperm(B, generator=torch.Generator().manual_seed(1)).to(torch_dev)
+    out3 = torch.empty_like(out)
+    s.solve_device(d_rec[perm].contiguous(), d_con[perm].contiguous(), out3, st)
+    torch.cuda.synchronize()
+    assert torch.equal(out3, out[perm])
+    # shard invariance: second half solved on its own
+    half = B // 2
+    out4 = torch.empty((B - half, H, 12), dtype=torch.float64, device=torch_dev)
+    s.solve_device(d_rec[half:].contiguous(), d_con[half:].contiguous(), out4, st[: B - half])
+    torch.cuda.synchronize()
+    assert torch.equal(out4, out[half:])
+    # oracle on a sample
+    idx = np.random.default_rng(cid).choice(B, 32, replace=False)
+    ref, _, _ = O.solve_batch(O.params_from(p), H, rec[idx], con[idx], n_threads=8)
+    assert rel_err(grf[idx], ref) <= TOL_REGRESS
+
+
+def test_device_path_equals_host_path(torch_dev):
+    import torch
+
+    p, H, rec, con = synth.config_batch(2, count=128)
+    s = BatchedConvexQPSolver(p, H, max_batch=128)
+    grf_h, st_h, it_h = s.solve(rec, con)
+    out = torch.empty((128, H, 12), dtype=torch.float64, device=torch_dev)
+    st = torch.empty(128, dtype=torch.int32, device=torch_dev)
+    it = torch.empty(128, dtype=torch.int32, device=torch_dev)
+    stream = torch.cuda.Stream(torch_dev)
+    s.solve_device(torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev), out, st, it, stream)
+    stream.synchronize()
+    assert np.array_equal(out.cpu().numpy(), grf_h)
+    assert np.array_equal(st.cpu().numpy(), st_h) and np.array_equal(it.cpu().numpy(), it_h)
+
+
+@pytest.mark.parametrize("H", [1, 2, 16, 17, 32])
+def test_horizon_range(H):
+    p = synth.params("go1")
+    rec, con = synth.fill(p, synth.synth_cfg("go1", -1), H, 12, seed=555 + H)
+    s = BatchedConvexQPSolver(p, H, max_batch=12)
+    grf, status, _ = s.solve(rec, con)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=4)
+    assert fails == 0 and np.all(status == 0)
+    assert rel_err(grf, ref) <= TOL_REGRESS
+
+
+def test_a1_params_and_standing_config():
+    p, H, rec, con = synth.config_batch(1)
+    s = BatchedConvexQPSolver(p, H, max_batch=1)
+    grf, status, _ = s.solve(rec, con)
+    ref, _, _ = O.solve(O.params_from(p), H, rec[0], con[0])
+    assert status[0] == 0 and rel_err(grf[0], ref) <= TOL_REGRESS
+    # standing with zero velocity: u_0 supports the weight (sum fz ~ m g), no lateral force
+    u0 = grf[0, 0].reshape(4, 3)
+    assert abs(u0[:, 2].sum() - p.robot_mass * p.gravity) < 0.5 * p.robot_mass * p.gravity
+
+
+def test_nan_input_returns_zeros_and_status():
+    p, H, rec, con = synth.config_batch(2, count=4)
+    rec = rec.copy()
+    rec[1, 5] = np.nan
+    s = BatchedConvexQPSolver(p, H, max_batch=4)
+    grf, status, _ = s.solve(rec, con)
+    assert status[1] == 2 and np.all(grf[1] == 0.0)
+    assert np.all(status[[0, 2, 3]] == 0)
+
+
+def test_empty_batch_and_all_swing():
+    p, H, rec, con = synth.config_batch(2, count=3)
+    s = BatchedConvexQPSolver(p, H, max_batch=3)
+    g0, s0, _ = s.solve(rec[:0], con[:0])
+    assert g0.shape == (0, H, 12)
+    con = con.copy()
+    con[:] = 0
+    grf, status, _ = s.solve(rec, con)
+    assert np.all(status == 0) and np.all(grf == 0.0)
+
+
+def test_reference_shaped_python_api():
+    """ConvexQPSolver used the way ConvexMpc::grf_update does (ConvexMpc.cpp:64-78)."""
+    from legged_mpc_control_amd import ConvexQPSolver, LeggedContactFSM, LeggedState
+
+    p = synth.params("go1")
+    st = LeggedState()
+    st.param.q_weights = np.array(p.q_weights[:])
+    st.param.gait_counter_speed = 4.0
+    st.fbk.root_pos = np.array([0.1, -0.2, 0.27])
+    st.fbk.root_euler = np.array([0.05, -0.03, 0.4])
+    c, s_ = np.cos(0.4), np.sin(0.4)
+    st.fbk.root_rot_mat = np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1.0]])
+    st.fbk.root_lin_vel = np.array([0.3, 0.0, 0.0])
+    st.fbk.foot_pos_abs = (st.fbk.root_rot_mat @ np.array(
+        [[0.17, 0.12, -0.3], [0.17, -0.17, -0.3], [-0.17, 0.17, -0.3], [-0.17, -0.12, -0.3]]).T)
+    st.ctrl.root_pos_d = np.array([0, 0, 0.28])
+    st.ctrl.root_lin_vel_d_rel = np.array([0.5, 0.1, 0.0])
+    st.ctrl.root_ang_vel_d_rel = np.array([0.0, 0.0, 0.3])
+    fsm = [LeggedContactFSM() for _ in range(4)]
+    for i in range(4):
+        fsm[i].reset_params(st, i)
+        fsm[i].gait_phase = 0.3
+        st.ctrl.plan_contacts[i] = bool(fsm[i].get_contact_state())
+    solver = ConvexQPSolver(p.q_weights, p.r_weights, horizon=10)
+    solver.calc_mpc_reference(st, fsm)
+    solver.update_cons_matrix()
+    u0 = solver.compute_grfs(st)
+    ref, _, _ = O.solve(O.params_from(p), 10, solver._rec[0], solver._con[0])
+    assert u0.shape == (12,) and solver.last_status == 0
+    assert rel_err(u0, ref[0]) <= TOL_REGRESS
+    np.testing.assert_allclose(st.ctrl.root_lin_vel_d_world, st.fbk.root_rot_mat @ st.ctrl.root_lin_vel_d_rel)
+
+
+def test_cpp_dropin_program_vs_oracle():
+    """tests/cpp/grf_update_test.cpp drives legged::ConvexQPSolver like ConvexMpc."""
+    from legged_mpc_control_amd import build as B
+
+    exe = B.build_cpp_test()
+    out = subprocess.run([exe, "10", "3"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.strip().splitlines()
+    p = synth.params("a1")
+    op = O.params_from(p)
+    ticks = 0
+    for i in range(0, len(lines), 5):
+        assert lines[i].endswith("status 0")
+        rec = np.array(lines[i + 1].split()[1:], dtype=np.float64)
+        con = np.array(lines[i + 2].split()[1:], dtype=np.uint8).reshape(10, 4)
+        grf = np.array(lines[i + 3].split()[1:], dtype=np.float64).reshape(10, 12)
+        u0 = np.array(lines[i + 4].split()[1:], dtype=np.float64)
+        ref, _, _ = O.solve(op, 10, rec, con)
+        assert rel_err(grf, ref) <= TOL_REGRESS
+        assert np.array_equal(u0, grf[0])
+        ticks += 1
+    assert ticks == 3
+
+
+def test_solve_options_and_status_codes():
+    from legged_mpc_control_amd import LmpcOptions
+    from legged_mpc_control_amd import _native as N
+
+    p, H, rec, con = synth.config_batch(2, count=32)
+    s = BatchedConvexQPSolver(p, H, max_batch=32)
+    o = LmpcOptions()
+    N.lib().lmpc_options_default(o)
+    o.max_iter, o.max_attempts = 2, 1  # far too few IPM iterations: polish may not verify
+    s.set_options(o)
+    grf, status, iters = s.solve(rec, con)
+    assert set(np.unique(status)) <= {0, 1}
+    assert np.all((iters & 0xFFFF) <= 2)
+    viol, _ = feasibility_violation(grf, con)
+    assert viol <= 1e-6 * p.f_max  # status-1 answers are the feasible interior-point iterate
+    N.lib().lmpc_options_default(o)
+    s.set_options(o)
+    grf, status, iters = s.solve(rec, con)
+    assert np.all(status == 0)

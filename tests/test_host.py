@@ -1,0 +1,125 @@
+"""CPU tests of the product's host-side path helpers: record packing
+(calc_mpc_reference), contact schedule (update_bound_constraints + FSM) and the
+seeded synthetic generator.  No GPU calls."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+
+from legged_mpc_control_amd import _native as N
+from legged_mpc_control_amd import synth
+from oracle import oracle as O
+
+
+def _pack_np(p, H, st):
+    """numpy restatement of ConvexQPSolver::calc_mpc_reference's state packing (:256-276)."""
+    R = np.asarray(st["R"])
+    vdw = R @ np.asarray(st["vd_rel"])
+    rec = np.zeros(33 + 12 * H)
+    rec[0:3], rec[3:6], rec[6:9], rec[9:12] = st["euler"], st["pos"], st["w"], st["v"]
+    rec[12:21] = R.reshape(9)
+    rec[21:33] = np.asarray(st["feet"]).reshape(12)
+    for i in range(H):
+        rec[33 + 12 * i:33 + 12 * i + 12] = [
+            st["euler_d"][0], st["euler_d"][1], st["euler"][2] + st["wd_rel"][2] * p.dt * i,
+            st["pos"][0] + vdw[0] * p.dt * i, st["pos"][1] + vdw[1] * p.dt * i, st["pos_d"][2],
+            st["wd_rel"][0], st["wd_rel"][1], st["wd_rel"][2], vdw[0], vdw[1], 0.0]
+    return rec, vdw
+
+
+def test_pack_record_matches_restatement():
+    rng = np.random.default_rng(3)
+    p = synth.params("go1")
+    for H in (1, 10, 30):
+        a = rng.uniform(-0.5, 0.5, 3)
+        c, s = np.cos(a[2]), np.sin(a[2])
+        st = dict(euler=a, pos=rng.normal(size=3), w=rng.normal(size=3), v=rng.normal(size=3),
+                  R=np.array([[c, -s, 0], [s, c, 0], [0, 0, 1.0]]), feet=rng.normal(size=(4, 3)) * 0.2,
+                  euler_d=rng.normal(size=3), pos_d=rng.normal(size=3), vd_rel=rng.normal(size=3),
+                  wd_rel=rng.normal(size=3))
+        si = N.LmpcStateIn()
+        si.root_euler[:] = list(st["euler"]); si.root_pos[:] = list(st["pos"])
+        si.root_ang_vel[:] = list(st["w"]); si.root_lin_vel[:] = list(st["v"])
+        si.root_rot_mat[:] = list(st["R"].reshape(9)); si.foot_pos_abs[:] = list(st["feet"].reshape(12))
+        si.root_euler_d[:] = list(st["euler_d"]); si.root_pos_d[:] = list(st["pos_d"])
+        si.root_lin_vel_d_rel[:] = list(st["vd_rel"]); si.root_ang_vel_d_rel[:] = list(st["wd_rel"])
+        rec = np.zeros(33 + 12 * H)
+        vdw = np.zeros(3)
+        dp = ctypes.POINTER(ctypes.c_double)
+        N.check(N.lib().lmpc_pack_record(ctypes.byref(p), H, ctypes.byref(si), rec.ctypes.data_as(dp),
+                                         vdw.ctypes.data_as(dp)))
+        want, wv = _pack_np(p, H, st)
+        np.testing.assert_allclose(rec, want, rtol=0, atol=1e-15)
+        np.testing.assert_allclose(vdw, wv, rtol=0, atol=1e-15)
+
+
+def test_contact_schedule_matches_fsm():
+    L = N.lib()
+    for gait in range(4):
+        for phase in (0.0, 0.13, 0.5, 0.77, 0.999):
+            plan = (np.arange(4) % 2).astype(np.uint8)
+            out = np.zeros((12, 4), dtype=np.uint8)
+            u8 = ctypes.POINTER(ctypes.c_uint8)
+            N.check(L.lmpc_contact_schedule(gait, phase, 4.0, 0.01, 12, plan.ctypes.data_as(u8), out.ctypes.data_as(u8)))
+            assert np.array_equal(out[0], plan)
+            for i in range(1, 12):
+                for j in range(4):
+                    assert out[i, j] == O.predict_contact(gait, j, phase, 4.0, 0.01 * i)
+
+
+def test_current_contact_is_fsm_state():
+    L = N.lib()
+    for gait in range(4):
+        for leg in range(4):
+            for ph in np.linspace(0, 0.999, 50):
+                assert L.lmpc_current_contact(gait, leg, ph) == O.current_contact(gait, leg, ph)
+
+
+def test_generator_deterministic_and_shard_invariant():
+    p = synth.params("go1")
+    cfg = synth.synth_cfg("go1", -1)
+    rec, con = synth.fill(p, cfg, 10, 64, seed=99)
+    rec2, con2 = synth.fill(p, cfg, 10, 64, seed=99)
+    assert np.array_equal(rec, rec2) and np.array_equal(con, con2)
+    # rank-style shards build exactly the same instances as the whole batch
+    for r in range(4):
+        rs, cs = synth.fill(p, cfg, 10, 16, seed=99, first_index=16 * r)
+        assert np.array_equal(rs, rec[16 * r:16 * r + 16]) and np.array_equal(cs, con[16 * r:16 * r + 16])
+    rec3, _ = synth.fill(p, cfg, 10, 64, seed=100)
+    assert not np.array_equal(rec, rec3)
+
+
+def test_generator_distributions():
+    """SURVEY.md 8d ranges: |roll|,|pitch| <= 0.2, p_z in [0.20, 0.35], z_d in [0.25, 0.32], R orthonormal."""
+    p, H, rec, con = synth.config_batch(2, count=2000)
+    assert np.all(np.abs(rec[:, 0:2]) <= 0.2)
+    assert np.all((rec[:, 5] >= 0.2) & (rec[:, 5] <= 0.35))
+    assert np.all((rec[:, 33 + 5] >= 0.25) & (rec[:, 33 + 5] <= 0.32))
+    R = rec[:, 12:21].reshape(-1, 3, 3)
+    assert np.allclose(R @ np.transpose(R, (0, 2, 1)), np.eye(3), atol=1e-12)
+    # trot: diagonal pairs, exactly two stance legs per step
+    assert np.all(con.sum(-1) == 2)
+    assert np.array_equal(con[..., 0], con[..., 3]) and np.array_equal(con[..., 1], con[..., 2])
+    # mixed gaits cover all four patterns (stand -> all four legs in stance for every step)
+    _, _, recm, conm = synth.config_batch(4, count=400)
+    assert np.any(np.all(conm == 1, axis=(1, 2)))
+
+
+@pytest.mark.parametrize("path", [p for p in golden_files() if "config" in p])
+def test_golden_inputs_pin_the_generator(path):
+    """The committed fixtures were generated by this generator; regenerate and compare."""
+    g = load_golden(path)
+    cid = int(path.split("golden_config")[1][0])
+    _, H, rec, con = synth.config_batch(cid, count=g["rec"].shape[0])
+    assert np.array_equal(rec, g["rec"]) and np.array_equal(con, g["contact"])
+
+
+def test_presets_match_reference_yaml():
+    p = synth.params("go1")  # gazebo_go1_convex.yaml:39-71
+    assert list(p.q_weights) == [50.0, 100.0, 0.0, 0.0, 0.0, 3500.0, 0.01, 0.01, 10.0, 15.0, 15.0, 20.0]
+    assert list(p.r_weights) == [1e-4] * 12
+    assert p.robot_mass == 13.0 and p.mu == 0.3 and p.f_max == 180.0 and p.gravity == 9.8 and p.dt == 0.01
+    a1 = synth.params("a1")  # gazebo_a1_convex.yaml:40-72
+    assert list(a1.q_weights) == [60.0, 100.0, 0.0, 0.0, 0.0, 450.0, 0.15, 0.15, 100.0, 3.0, 3.0, 5.0]
