@@ -91,10 +91,11 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB_PATH):
+        path = os.environ.get("LMPC_LIB") or LIB_PATH  # LMPC_LIB: diagnostic builds (tools/) only
+        if not os.path.exists(path):
             raise NativeLibraryError(
-                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-        L = ctypes.CDLL(LIB_PATH)
+                f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(path)
         vp, dp, i32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
         u8p = ctypes.POINTER(ctypes.c_uint8)
         pp = ctypes.POINTER(LmpcParams)

@@ -43,6 +43,20 @@
 namespace lmpc {
 
 #define LMPC_SYNC() __syncthreads()
+
+// Diagnostic build only (-DLMPC_STAMPS): per-phase cycle counters of QP 0..STAMP_QPS-1,
+// written to a buffer no other code reads.  Never compiled into the product library.
+#ifdef LMPC_STAMPS
+constexpr int STAMP_QPS = 4096;
+__device__ unsigned long long lmpc_stamps[STAMP_QPS][8];
+#define STAMP_DECL unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long _st_t0 = __builtin_readcyclecounter();
+#define STAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _st_acc[i] += _t - _st_t0; _st_t0 = _t; } while (0)
+#define STAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < STAMP_QPS) for (int _i = 0; _i < 8; ++_i) lmpc_stamps[qp][_i] = _st_acc[_i]; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH(qp) do {} while (0)
+#endif
 // Explicit LDS address space: every shared access compiles to ds_read/ds_write
 // (a generic pointer would fall back to flat_load/flat_store).
 typedef __attribute__((address_space(3))) double ldouble;
@@ -709,6 +723,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     const Smem S = carve(lmpc_smem, H);
     double* gs = scratch + (size_t)qp * GS * H;
     const double mu = prm.mu, fzmax = prm.fmax, dt = prm.dt;
+    STAMP_DECL
 
     // ---- load the record (coalesced, one pass) ----
     const double* rin = rec + (size_t)qp * RL;
@@ -792,6 +807,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         u[t][0] = u[t][1] = u[t][2] = 0.0;
     }
     const double nst = wave_sum((double)nst_loc);
+    STAMP(0);  // prologue
     int qstatus = LMPC_QP_CONVERGED;
     int ipm_it = 0, prounds = 0;
     bool done = false;
@@ -881,8 +897,11 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
             if (mode != CORR) leg_stage_prep<LS>(prm, S, valid, lsk, lsj, Rt, T, up);
             leg_rhs<LS>(S, valid, lsk, lsj, Rt, rt, T, up);
             LMPC_SYNC();
+            STAMP(1);  // leg-step work (IPM/polish bookkeeping, stage prep)
             if (mode != CORR) riccati_factor(prm, S, gs, lane);
+            STAMP(2);  // factorisation
             riccati_solve(prm, S, gs, lane);
+            STAMP(3);  // vector pass
             leg_u<LS>(S, valid, lsk, lsj, T, up, u);
             if (mode == PRED) {
                 double amax = 1.0;
@@ -956,7 +975,9 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                 mode = PRED;
             } else {
                 // ---- polish verification: primal feasibility + multiplier signs ----
+                STAMP(1);
                 adjoint(prm, S, lane);
+                STAMP(4);  // adjoint
                 double g[LS][3];
                 double gloc = 1.0;
 #pragma unroll
@@ -1065,6 +1086,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
             u[t][2] = f[t][2];
         }
     }
+    STAMP(1);
     // ---- NaN guard (reference: NaN -> zeros, ConvexQPSolver.cpp:321-326) and output ----
     int bad = 0;
 #pragma unroll
@@ -1079,6 +1101,8 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
 #pragma unroll
         for (int p = 0; p < 3; ++p) gout[3 * ls + p] = (anybad || !st[t]) ? 0.0 : u[t][p];
     }
+    STAMP(5);  // epilogue
+    STAMP_FLUSH(qp);
     if (lane == 0) {
         if (status) status[qp] = anybad ? LMPC_QP_NAN : qstatus;
         if (iters) iters[qp] = ipm_it | (prounds << 16);
@@ -1106,5 +1130,12 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
     }
     return hipGetLastError();
 }
+
+#ifdef LMPC_STAMPS
+extern "C" int lmpc_debug_stamps(unsigned long long* out, int nqp) {
+    if (nqp > STAMP_QPS) nqp = STAMP_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_stamps), (size_t)nqp * 8 * sizeof(unsigned long long)) == hipSuccess ? nqp : -1;
+}
+#endif
 
 }  // namespace lmpc

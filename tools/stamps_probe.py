@@ -1,0 +1,25 @@
+"""Dev tool: per-phase cycle breakdown from the -DLMPC_STAMPS diagnostic build (run under gpurun)."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from legged_mpc_control_amd import build as B
+os.environ["LMPC_LIB"] = B.build_stamps()
+import numpy as np
+from legged_mpc_control_amd import BatchedConvexQPSolver, synth
+from legged_mpc_control_amd import _native as N
+
+cid = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+count = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+p, H, rec, con = synth.config_batch(cid, count=count)
+s = BatchedConvexQPSolver(p, H, max_batch=count)
+for _ in range(2):
+    grf, st, it = s.solve(rec, con)
+L = N.lib()
+L.lmpc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = np.zeros((min(count, 4096), 8), dtype=np.uint64)
+n = L.lmpc_debug_stamps(buf.ctypes.data, buf.shape[0])
+names = ["prologue", "leg/ipm", "factor", "solve", "adjoint", "epilogue"]
+tot = buf[:n, :6].sum(1).astype(float)
+print(f"config {cid} H={H} B={count}: mean cycles/QP {tot.mean():.0f}  ipm_it {np.mean(it & 0xffff):.2f} rounds {np.mean(it >> 16):.2f}")
+for i, nm in enumerate(names):
+    print(f"  {nm:9s} {buf[:n, i].astype(float).mean():12.0f}  ({100 * buf[:n, i].astype(float).mean() / tot.mean():5.1f}%)")
