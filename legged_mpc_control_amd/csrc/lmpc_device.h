@@ -24,10 +24,12 @@ struct DevParams {
     int max_attempts;  // IPM+polish attempts (tol_mu tightened x1e-3 per attempt)
 };
 
-// LDS footprint (doubles) of one QP for horizon H; must match carve() in lmpc_kernels.hip.
-inline int lds_doubles(int H) { return 1058 + 14 * H + 276 * H; }
+// LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
+constexpr int LDS_FIXED_DOUBLES = 916;  // per-QP matrices and buffers
+constexpr int LDS_STAGE_DOUBLES = 282;  // per-stage slot (SK)
+inline int lds_doubles(int H) { return LDS_FIXED_DOUBLES + 14 * H + LDS_STAGE_DOUBLES * H; }
 inline size_t lds_bytes(int H) { return (size_t)lds_doubles(H) * sizeof(double); }
-// Global scratch (doubles) per QP: L^-1, V, K, P2 per stage (GS = 243).
-inline size_t scratch_doubles_per_qp(int H) { return (size_t)243 * H; }
+// Global scratch (doubles) per QP: L^-1, V, K, Z per stage (GS = 258).
+inline size_t scratch_doubles_per_qp(int H) { return (size_t)258 * H; }
 
 }  // namespace lmpc

@@ -52,7 +52,16 @@ __device__ unsigned long long lmpc_stamps[STAMP_QPS][8];
 #define STAMP_DECL unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long _st_t0 = __builtin_readcyclecounter();
 #define STAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _st_acc[i] += _t - _st_t0; _st_t0 = _t; } while (0)
 #define STAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < STAMP_QPS) for (int _i = 0; _i < 8; ++_i) lmpc_stamps[qp][_i] = _st_acc[_i]; } while (0)
+// sub-phase stamps inside the outlined factor / solve functions (slot < 16)
+__device__ unsigned long long lmpc_substamps[STAMP_QPS][16];
+#define SUB_DECL unsigned long long _sb_t0 = __builtin_readcyclecounter();
+#define SUB(i) do { const unsigned long long _t = __builtin_readcyclecounter(); \
+    if (threadIdx.x == 0 && blockIdx.x < STAMP_QPS) \
+        __hip_atomic_fetch_add(&lmpc_substamps[blockIdx.x][i], _t - _sb_t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    _sb_t0 = _t; } while (0)
 #else
+#define SUB_DECL
+#define SUB(i) do {} while (0)
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH(qp) do {} while (0)
@@ -60,6 +69,8 @@ __device__ unsigned long long lmpc_stamps[STAMP_QPS][8];
 // Explicit LDS address space: every shared access compiles to ds_read/ds_write
 // (a generic pointer would fall back to flat_load/flat_store).
 typedef __attribute__((address_space(3))) double ldouble;
+// Explicit global address space for the per-QP scratch (outlined functions would otherwise use flat ops).
+typedef __attribute__((address_space(1))) double gdouble;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -132,17 +143,17 @@ constexpr int SO_VV = 198;   // 12  v = P_{k+1} d_k
 constexpr int SO_CST = 210;  // 12  q_k - Z' psi
 constexpr int SO_PSI = 222;  // 6   V' L^-1 rr
 constexpr int SO_RHO = 228;  // 12  L^-1 rr (later: t)
-constexpr int SO_S2 = 240;   // 6   (v + p_{k+1})[6:12]
-constexpr int SO_N6 = 246;   // 6   K s2 + psi (later: q2)
-constexpr int SO_XS = 252;   // 12  x_k
-constexpr int SO_LAM = 264;  // 12  lambda_{k+1}
-constexpr int SK = 276;
+constexpr int SO_N6 = 240;   // 6   K s2 + psi - dv (later: q2)
+constexpr int SO_PN = 246;   // 12  p_{k+1}
+constexpr int SO_XS = 258;   // 12  x_k
+constexpr int SO_LAM = 270;  // 12  lambda_{k+1}
+constexpr int SK = 282;
 // global scratch per stage
-constexpr int GO_LINV = 0;   // 78 packed L^-1
-constexpr int GO_V = 78;     // 12 x 6 V = L^-1 Bt'
-constexpr int GO_K = 150;    // 21 packed K
-constexpr int GO_P2 = 171;   // 6 x 12 rows 6..11 of P_{k+1}
-constexpr int GS = 243;
+constexpr int GO_LINV = 0;   // 78 packed L^-1 (lower, row-packed)
+constexpr int GO_V = 78;     // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
+constexpr int GO_K = 150;    // 6 x 6 K = V'V
+constexpr int GO_Z = 186;    // 6 x 12 Z = P2_{k+1} A_k
+constexpr int GS = 258;
 
 struct Smem {
     ldouble* G0;   // 72
@@ -150,52 +161,68 @@ struct Smem {
     ldouble* cs;   // 2H
     ldouble* xr;   // 12H
     ldouble* xH;   // 12
-    ldouble* P;    // 144
-    ldouble* APA;  // 144
+    ldouble* P;    // 144  P_{k+1}
+    ldouble* Pn;   // 144  P_k (double buffer)
     ldouble* C;    // 72   P22 Bt
-    ldouble* Z;    // 72   P2 A
-    ldouble* G;    // 144  Guu -> L
-    ldouble* RV;   // 12 x 18  [Bt' | I] -> [V | L^-1]
-    ldouble* LP;   // 27   panel
-    ldouble* XB;   // 54   panel rhs rows
+    ldouble* PA6;  // 72   columns 6..11 of P A  (rows 6..11 = columns 6..11 of Z)
+    ldouble* GT;   // 144  Guu, column-major
+    ldouble* PNL;  // 72   pivot block columns (3 columns x 12 rows), double-buffered
+    ldouble* VL;   // 72   V = L^-1 Bt', column-major
     ldouble* K;    // 36
     ldouble* pa;   // 12
     ldouble* pb;   // 12
+    ldouble* qw;   // 12  state weights q
     ldouble* st;   // H * SK
 };
+
+// fixed-size LDS members, in carve order; the total must equal LDS_FIXED_DOUBLES (lmpc_device.h)
+constexpr int LDS_SIZES[] = {72, 40, 12, 144, 144, 72, 72, 144, 72, 72, 36, 12, 12, 12};
+constexpr int lds_fixed_sum() {
+    int t = 0;
+    for (int v : LDS_SIZES) t += v;
+    return t;
+}
+static_assert(lds_fixed_sum() == LDS_FIXED_DOUBLES, "LDS carve and lds_doubles() disagree");
+static_assert(SK == LDS_STAGE_DOUBLES, "per-stage LDS slot and lds_doubles() disagree");
 
 __device__ __forceinline__ Smem carve(double* sm, int H) {
     Smem s;
     ldouble* p = (ldouble*)sm;
     s.G0 = p; p += 72;
     s.hdr = p; p += 40;
-    s.cs = p; p += 2 * H;
-    s.xr = p; p += 12 * H;
     s.xH = p; p += 12;
     s.P = p; p += 144;
-    s.APA = p; p += 144;
+    s.Pn = p; p += 144;
     s.C = p; p += 72;
-    s.Z = p; p += 72;
-    s.G = p; p += 144;
-    s.RV = p; p += 216;
-    s.LP = p; p += 28;
-    s.XB = p; p += 54;
+    s.PA6 = p; p += 72;
+    s.GT = p; p += 144;
+    s.PNL = p; p += 72;
+    s.VL = p; p += 72;
     s.K = p; p += 36;
     s.pa = p; p += 12;
     s.pb = p; p += 12;
-    s.st = p;  // offset 1058 + 14H doubles (even: 16-B aligned)
+    s.qw = p; p += 12;
+    s.cs = p; p += 2 * H;
+    s.xr = p; p += 12 * H;
+    s.st = p;  // offset LDS_FIXED_DOUBLES + 14H doubles (even: 16-B aligned)
     return s;
 }
 
-// (P N)[r][c] with N the nilpotent part of A = I + dt N
-template <class Ptr>
-__device__ __forceinline__ double PNel(Ptr P, int r, int c, double ck, double sk) {
-    if (c >= 6 && c < 9) {
-        return P[r * 12 + 0] * Myaw(ck, sk, 0, c - 6) + P[r * 12 + 1] * Myaw(ck, sk, 1, c - 6) +
-               P[r * 12 + 2] * Myaw(ck, sk, 2, c - 6);
-    }
-    if (c >= 9) return P[r * 12 + c - 6];
-    return 0.0;
+// 1/sqrt(x) to full fp64 precision: hardware estimate + two Newton steps
+// (cheaper than the correctly-rounded sqrt + divide sequences).
+__device__ __forceinline__ double rsq_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+// M(yaw)[i][j] for a lane-static j and per-stage (c, s)
+__device__ __forceinline__ void Mcol(double c, double s, int j, double m[3]) {
+    m[0] = (j == 0) ? c : (j == 1) ? s : 0.0;
+    m[1] = (j == 0) ? -s : (j == 1) ? c : 0.0;
+    m[2] = (j == 2) ? 1.0 : 0.0;
 }
 
 // (A x)[c] for the stage yaw (c, s)
@@ -216,320 +243,442 @@ __device__ __forceinline__ double Atw_el(Ptr w, int r, double ck, double sk, dou
 }
 
 // ---------------------------------------------------------------------------
-// Riccati factorisation (backward, matrix part)
+// Riccati factorisation (backward, matrix part).
+//
+// Every lane has a fixed role per level (no task loops, no index decoding on
+// the critical path); 13 barriers per stage:
+//   A  C = P22 Bt (lanes 0-23) | PA6 = (P A)[:, 6:12] (24-47) | v = P d (48-59)
+//   B  Guu = blockdiag(Rr) + Bt' C, written column-major (lanes 0-47)
+//   elimination of [Guu | Bt' | I] by 3x3 leg blocks: lane j < 30 keeps column j
+//      in registers; per block: the pivot columns go to LDS, every lane factors
+//      the 3x3 pivot (rsq + Newton), lanes < 27 form the panel L_ba, every
+//      column lane applies it  -> V = L^-1 Bt' (lanes 12-17), L^-1 (lanes 18-29)
+//   D  K = V'V (lanes 0-35)
+//   E  KZ = K Z, Z = P2 A = [P2[:, 0:6] | PA6[6:12]] (lanes 0-23)
+//   F  P_k = Q + A'PA - Z'(KZ) into the other P buffer (lanes 0-47), with
+//      A'PA assembled from P and PA6 (A = I + dt N touches 6 columns / rows only)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void riccati_factor(const DevParams& prm, const Smem& S, double* __restrict__ gs, int lane) {
-    const int H = prm.H;
-    const double dt = prm.dt;
-    for (int e = lane; e < 144; e += 64) S.P[e] = (e % 13 == 0) ? prm.q[e / 13] : 0.0;
+__device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, const int H, const double dt,
+                                                         const int lane) {
+    // lane-static roles
+    const int qr = lane >> 2, qg = lane & 3;              // row / 3-column group of a 12-wide output
+    const int tA = lane - 24, rA = tA >> 1, cgA = tA & 1;  // PA6 task (lanes 24-47)
+    const int dm = lane / 6, dn = lane - 6 * (lane / 6);   // K task (lanes 0-35)
+    const int qr3 = qr / 3, qrm3 = qr - 3 * (qr / 3);
+    const double qq = S.qw[qr < 12 ? qr : 0];
+    const double qdiag[3] = {(qr == 3 * qg) ? qq : 0.0, (qr == 3 * qg + 1) ? qq : 0.0, (qr == 3 * qg + 2) ? qq : 0.0};
+    ldouble* P = S.P;
+    ldouble* Pn = S.Pn;
+    for (int e = lane; e < 144; e += 64) P[e] = (e % 13 == 0) ? S.qw[e / 13] : 0.0;
     LMPC_SYNC();
+    SUB_DECL
     for (int k = H - 1; k >= 0; --k) {
         const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
         ldouble* sl = S.st + k * SK;
-        double* g = gs + k * GS;
+        gdouble* g = gs + k * GS;
         const ldouble* Bt = sl + SO_BT;
-        // ---- level A: C = P22 Bt, Z = P2 A (+P2 -> global), v = P d, APA = A'PA ----
-        for (int e = lane; e < 72 + 72 + 12 + 78; e += 64) {
-            if (e < 72) {
-                const int m = e / 12, c = e % 12;
+        // ---- level A ----
+        if (lane < 24) {
+            double p[6];
+#pragma unroll
+            for (int n = 0; n < 6; ++n) p[n] = P[(6 + qr) * 12 + 6 + n];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
                 double v = 0.0;
 #pragma unroll
-                for (int n = 0; n < 6; ++n) v += S.P[(6 + m) * 12 + 6 + n] * Bt[n * 12 + c];
-                S.C[e] = v;
-            } else if (e < 144) {
-                const int e2 = e - 72, m = e2 / 12, c = e2 % 12;
-                const double p = S.P[(6 + m) * 12 + c];
-                S.Z[e2] = p + dt * PNel(S.P, 6 + m, c, ck, sk);
-                g[GO_P2 + e2] = p;
-            } else if (e < 156) {
-                const int r = e - 144;
-                double v = 0.0;
-#pragma unroll
-                for (int n = 0; n < 6; ++n) v += S.P[r * 12 + 6 + n] * sl[SO_DV + n];
-                sl[SO_VV + r] = v;
-            } else {
-                // lower-triangle entry (r, c) of A'PA = P + dt(PN + N'P) + dt^2 N'PN
-                int r, c;
-                unpk(e - 156, r, c);
-                double v = S.P[r * 12 + c] + dt * (PNel(S.P, r, c, ck, sk) + PNel(S.P, c, r, ck, sk));
-                double npn = 0.0;
-                if (r >= 6 && r < 9) {
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) npn += Myaw(ck, sk, i, r - 6) * PNel(S.P, i, c, ck, sk);
-                } else if (r >= 9) {
-                    npn = PNel(S.P, r - 6, c, ck, sk);
-                }
-                v += dt * dt * npn;
-                S.APA[r * 12 + c] = v;
-                S.APA[c * 12 + r] = v;
+                for (int n = 0; n < 6; ++n) v += p[n] * Bt[n * 12 + 3 * qg + i];
+                S.C[qr * 12 + 3 * qg + i] = v;
             }
-        }
-        LMPC_SYNC();
-        // ---- level B: Guu = blockdiag(Rr) + Bt' C (lower) ----
-        for (int e = lane; e < 78; e += 64) {
-            int r, c;
-            unpk(e, r, c);
+            if (qg < 2) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) g[GO_Z + qr * 12 + 3 * qg + i] = P[(6 + qr) * 12 + 3 * qg + i];
+            }
+        } else if (lane < 48) {
+            // PA6[r][3cg+i] = P[r][6+3cg+i] + dt sum_q P[r][3cg+q] W[q][i],  W = M(yaw) (cg 0) or I (cg 1)
+            double b[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) b[q] = P[rA * 12 + 3 * cgA + q];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                double m[3];
+                Mcol(ck, sk, i, m);
+                if (cgA) {
+                    m[0] = (i == 0) ? 1.0 : 0.0;
+                    m[1] = (i == 1) ? 1.0 : 0.0;
+                    m[2] = (i == 2) ? 1.0 : 0.0;
+                }
+                const double v = P[rA * 12 + 6 + 3 * cgA + i] + dt * (b[0] * m[0] + b[1] * m[1] + b[2] * m[2]);
+                S.PA6[rA * 6 + 3 * cgA + i] = v;
+                if (rA >= 6) g[GO_Z + (rA - 6) * 12 + 6 + 3 * cgA + i] = v;
+            }
+        } else if (lane < 60) {
+            const int r = lane - 48;
             double v = 0.0;
 #pragma unroll
-            for (int m = 0; m < 6; ++m) v += Bt[m * 12 + r] * S.C[m * 12 + c];
-            if (r / 3 == c / 3) v += sl[SO_RR + (r / 3) * 9 + (r % 3) * 3 + (c % 3)];
-            S.G[r * 12 + c] = v;
+            for (int n = 0; n < 6; ++n) v += P[r * 12 + 6 + n] * sl[SO_DV + n];
+            sl[SO_VV + r] = v;
         }
         LMPC_SYNC();
-        // ---- levels C: block Cholesky by legs, RHS [Bt' | I] eliminated alongside ----
-        for (int a = 0; a < 4; ++a) {
-            const int o = 3 * a;
-            const double g00 = S.G[o * 12 + o], g10 = S.G[(o + 1) * 12 + o], g11 = S.G[(o + 1) * 12 + o + 1];
-            const double g20 = S.G[(o + 2) * 12 + o], g21 = S.G[(o + 2) * 12 + o + 1], g22 = S.G[(o + 2) * 12 + o + 2];
-            const double l00 = sqrt(g00), i00 = 1.0 / l00;
-            const double l10 = g10 * i00, l20 = g20 * i00;
-            const double l11 = sqrt(g11 - l10 * l10), i11 = 1.0 / l11;
-            const double l21 = (g21 - l20 * l10) * i11;
-            const double l22 = sqrt(g22 - l20 * l20 - l21 * l21), i22 = 1.0 / l22;
-            // Lai = L_aa^-1 (lower)
-            const double m10 = -l10 * i00 * i11;
-            const double m21 = -l21 * i11 * i22;
-            const double m20 = -(l20 * i00 + l21 * m10) * i22;
-            const double Lai[3][3] = {{i00, 0.0, 0.0}, {m10, i11, 0.0}, {m20, m21, i22}};
-            const int npan = 9 * (3 - a);
-            // panel: L_ba = G_ba L_aa^-T (b > a), X_a = L_aa^-1 RHS_a
-            for (int e = lane; e < npan + 54; e += 64) {
-                if (e < npan) {
-                    const int bb = a + 1 + e / 9, i = (e % 9) / 3, j = e % 3;
-                    // L_ba[i][j] = sum_{q<=j} G_ba[i][q] Lai[j][q]  (Lai lower: zero above the diagonal)
-                    const double w0 = (j == 0) ? Lai[0][0] : (j == 1) ? Lai[1][0] : Lai[2][0];
-                    const double w1 = (j == 0) ? 0.0 : (j == 1) ? Lai[1][1] : Lai[2][1];
-                    const double w2 = (j == 2) ? Lai[2][2] : 0.0;
-                    const int gr = (3 * bb + i) * 12 + o;
-                    S.LP[e] = S.G[gr] * w0 + S.G[gr + 1] * w1 + S.G[gr + 2] * w2;
-                } else {
-                    const int e2 = e - npan, i = e2 / 18, c = e2 % 18;
-                    double rhs[3];
+        SUB(5);
+        // ---- level B: Guu (all 144 entries), column-major ----
+        if (lane < 48) {
+            double bt[6];
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const int row = o + q;
-                        rhs[q] = (a == 0) ? ((c < 6) ? Bt[c * 12 + row] : (c - 6 == row ? 1.0 : 0.0)) : S.RV[row * 18 + c];
-                    }
-                    const double w0 = (i == 0) ? Lai[0][0] : (i == 1) ? Lai[1][0] : Lai[2][0];
-                    const double w1 = (i == 0) ? 0.0 : (i == 1) ? Lai[1][1] : Lai[2][1];
-                    const double w2 = (i == 2) ? Lai[2][2] : 0.0;
-                    S.XB[e2] = w0 * rhs[0] + w1 * rhs[1] + w2 * rhs[2];
-                }
-            }
-            LMPC_SYNC();
-            // trailing update of G (lower blocks b >= c > a) and RHS rows b > a
-            const int nb = 3 - a;
-            const int ntr = 9 * nb * (nb + 1) / 2;
-            const int nrv = 54 * nb;
-            for (int e = lane; e < ntr + nrv; e += 64) {
-                if (e < ntr) {
-                    int blk = e / 9, b2 = a + 1, c2 = a + 1;
-                    while (blk > 0) {
-                        if (c2 < b2) ++c2;
-                        else { ++b2; c2 = a + 1; }
-                        --blk;
-                    }
-                    const int i = (e % 9) / 3, j = e % 3;
-                    const ldouble* Lb = S.LP + (b2 - a - 1) * 9;
-                    const ldouble* Lc = S.LP + (c2 - a - 1) * 9;
-                    double v = S.G[(3 * b2 + i) * 12 + 3 * c2 + j];
+            for (int m = 0; m < 6; ++m) bt[m] = Bt[m * 12 + qr];
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) v -= Lb[i * 3 + q] * Lc[j * 3 + q];
-                    S.G[(3 * b2 + i) * 12 + 3 * c2 + j] = v;
-                } else {
-                    const int e2 = e - ntr, b2 = a + 1 + e2 / 54, i = (e2 % 54) / 18, c = e2 % 18;
-                    const int row = 3 * b2 + i;
-                    const ldouble* Lb = S.LP + (b2 - a - 1) * 9;
-                    double v = (a == 0) ? ((c < 6) ? Bt[c * 12 + row] : (c - 6 == row ? 1.0 : 0.0)) : S.RV[row * 18 + c];
+            for (int i = 0; i < 3; ++i) {
+                double v = (qr3 == qg) ? sl[SO_RR + qg * 9 + qrm3 * 3 + i] : 0.0;
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) v -= Lb[i * 3 + q] * S.XB[q * 18 + c];
-                    S.RV[row * 18 + c] = v;
-                }
-            }
-            // commit X_a -> RV rows o..o+2 (final rows of [V | L^-1]); rows > o+2 only touched above
-            for (int e = lane; e < 54; e += 64) S.RV[(o + e / 18) * 18 + e % 18] = S.XB[e];
-            LMPC_SYNC();
-        }
-        // ---- level D: K = V'V ; store L^-1, V, K to the global scratch ----
-        for (int e = lane; e < 21 + 78 + 72; e += 64) {
-            if (e < 21) {
-                int m, n;
-                unpk(e, m, n);
-                double v = 0.0;
-#pragma unroll
-                for (int r = 0; r < 12; ++r) v += S.RV[r * 18 + m] * S.RV[r * 18 + n];
-                S.K[m * 6 + n] = v;
-                S.K[n * 6 + m] = v;
-                g[GO_K + e] = v;
-            } else if (e < 99) {
-                int r, c;
-                unpk(e - 21, r, c);
-                g[GO_LINV + e - 21] = S.RV[r * 18 + 6 + c];
-            } else {
-                const int e2 = e - 99;
-                g[GO_V + e2] = S.RV[(e2 / 6) * 18 + e2 % 6];
+                for (int m = 0; m < 6; ++m) v += bt[m] * S.C[m * 12 + 3 * qg + i];
+                S.GT[(3 * qg + i) * 12 + qr] = v;
             }
         }
         LMPC_SYNC();
+        SUB(6);
+        // ---- block Cholesky elimination of [Guu | Bt' | I] -> [L' | V = L^-1 Bt' | L^-1] ----
+        // lane j < 30 keeps column j in registers.  Per 3x3 leg block (one barrier each):
+        // the pivot columns go to LDS; every lane factors the pivot block D = Ld Ld' itself,
+        // keeps z = Ld^-1 x as its final block rows and subtracts G_rb D^-1 x = G_rb Ld^-T z
+        // from the rows below, reading G_rb straight from the pivot columns.
+        double a[12];
+        {
+            const ldouble* src = (lane < 12) ? S.GT + 12 * lane : Bt + 12 * (lane < 18 ? lane - 12 : 0);
+            const double keep = (lane < 18) ? 1.0 : 0.0;  // blend, not select: keeps the loads unconditional
+#pragma unroll
+            for (int r = 0; r < 12; ++r) a[r] = fma(src[r], keep, (r == lane - 18) ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+            const int o = 3 * blk;
+            ldouble* pnl = S.PNL + (blk & 1) * 36;  // double-buffered: block b+1 writes while nobody reads block b's copy
+            if (lane >= o && lane < o + 3) {
+#pragma unroll
+                for (int r = o; r < 12; ++r) pnl[(lane - o) * 12 + r] = a[r];
+            }
+            LMPC_SYNC();
+            const double i00 = rsq_nr(pnl[o]);
+            const double l10 = pnl[o + 1] * i00, l20 = pnl[o + 2] * i00;
+            const double i11 = rsq_nr(pnl[12 + o + 1] - l10 * l10);
+            const double l21 = (pnl[12 + o + 2] - l20 * l10) * i11;
+            const double i22 = rsq_nr(pnl[24 + o + 2] - l20 * l20 - l21 * l21);
+            const double z0 = i00 * a[o];
+            const double z1 = (a[o + 1] - l10 * z0) * i11;
+            const double z2 = (a[o + 2] - l20 * z0 - l21 * z1) * i22;
+            if (blk < 3) {
+                const double y2 = z2 * i22;
+                const double y1 = (z1 - l21 * y2) * i11;
+                const double y0 = (z0 - l10 * y1 - l20 * y2) * i00;
+#pragma unroll
+                for (int r = o + 3; r < 12; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
+            }
+            a[o] = z0;
+            a[o + 1] = z1;
+            a[o + 2] = z2;
+        }
+        // V (lanes 12-17) and L^-1 (lanes 18-29) out
+        if (lane >= 12 && lane < 18) {
+#pragma unroll
+            for (int r = 0; r < 12; ++r) {
+                S.VL[(lane - 12) * 12 + r] = a[r];
+                g[GO_V + (lane - 12) * 12 + r] = a[r];
+            }
+        } else if (lane >= 18 && lane < 30) {
+            const int c = lane - 18;
+#pragma unroll
+            for (int r = 0; r < 12; ++r)
+                if (r >= c) g[GO_LINV + r * (r + 1) / 2 + c] = a[r];
+        }
+        LMPC_SYNC();
+        SUB(7);
+        // ---- level D: K = V'V ----
+        if (lane < 36) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < 12; ++r) v += S.VL[dm * 12 + r] * S.VL[dn * 12 + r];
+            S.K[lane] = v;
+            g[GO_K + lane] = v;
+        }
+        LMPC_SYNC();
+        SUB(8);
         // ---- level E: KZ = K Z ----
-        for (int e = lane; e < 72; e += 64) {
-            const int m = e / 12, c = e % 12;
-            double v = 0.0;
+        if (lane < 24) {
+            const bool lo = qg < 2;
+            const ldouble* zb = lo ? P + 72 + 3 * qg : S.PA6 + 36 + 3 * (qg - 2);
+            const int zs = lo ? 12 : 6;
+            double kk[6];
 #pragma unroll
-            for (int n = 0; n < 6; ++n) v += S.K[m * 6 + n] * S.Z[n * 12 + c];
-            sl[SO_KZ + e] = v;
+            for (int n = 0; n < 6; ++n) kk[n] = S.K[qr * 6 + n];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                double v = 0.0;
+#pragma unroll
+                for (int n = 0; n < 6; ++n) v += kk[n] * zb[n * zs + i];
+                sl[SO_KZ + qr * 12 + 3 * qg + i] = v;
+            }
         }
         LMPC_SYNC();
+        SUB(9);
         // ---- level F: P_k = Q + A'PA - Z'(KZ) ----
         if (k > 0) {
-            for (int e = lane; e < 78; e += 64) {
-                int r, c;
-                unpk(e, r, c);
-                double v = S.APA[r * 12 + c] + (r == c ? prm.q[r] : 0.0);
+            if (lane < 48) {
+                const bool rlo = qr < 6, clo = qg < 2;
+                // Z[m][qr]
+                const ldouble* zr = rlo ? P + 72 + qr : S.PA6 + 36 + (qr - 6);
+                const int zs = rlo ? 12 : 6;
+                double zc[6];
 #pragma unroll
-                for (int m = 0; m < 6; ++m) v -= S.Z[m * 12 + r] * sl[SO_KZ + m * 12 + c];
-                S.P[r * 12 + c] = v;
-                S.P[c * 12 + r] = v;
+                for (int m = 0; m < 6; ++m) zc[m] = zr[m * zs];
+                // A'PA[qr][3qg+i]
+                const ldouble* ab;
+                int as;
+                if (clo) {
+                    ab = rlo ? P + qr * 12 + 3 * qg : S.PA6 + 3 * qg * 6 + (qr - 6);
+                    as = rlo ? 1 : 6;
+                } else {
+                    ab = S.PA6 + qr * 6 + 3 * (qg - 2);
+                    as = 1;
+                }
+                // bottom-right block: + dt sum_q Wr[q] PA6[3rg+q][c-6]
+                const bool br = !rlo && !clo;
+                const int rp = rlo ? 0 : qr - 6, rg = rp / 3;
+                double wr[3];
+                Mcol(ck, sk, rp, wr);  // M[q][rp] for rp < 3
+                if (rg) {
+                    wr[0] = (rp == 3) ? 1.0 : 0.0;
+                    wr[1] = (rp == 4) ? 1.0 : 0.0;
+                    wr[2] = (rp == 5) ? 1.0 : 0.0;
+                }
+                const ldouble* cb = S.PA6 + (br ? 3 * rg * 6 + 3 * (qg - 2) : 0);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    double v = ab[i * as] + qdiag[i];
+                    const double corr = cb[i] * wr[0] + cb[6 + i] * wr[1] + cb[12 + i] * wr[2];
+                    v += br ? dt * corr : 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) v -= zc[m] * sl[SO_KZ + m * 12 + 3 * qg + i];
+                    Pn[qr * 12 + 3 * qg + i] = v;
+                }
             }
             LMPC_SYNC();
+            SUB(10);
+            ldouble* t = P;
+            P = Pn;
+            Pn = t;
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// Vector pass: pre-pass, backward/forward affine recursions, post-pass.
-// Reads SO_RRV (rr) per stage; leaves y (12 per stage) in SO_RRV and x_k in SO_XS / xH.
+// Vector pass.  Reads rr (SO_RRV) per stage; leaves y in SO_RRV and x_k in SO_XS / xH.
+//   pre   rho = L^-1 rr ; psi = V' rho ; cst'_k = q_k - Z'psi + A'v - (KZ)'v6
+//   back  p_k = A'p_{k+1} - (KZ)' p_{k+1}[6:12] + cst'_k          (serial, lanes 0-11)
+//   mid   n6'_k = K (v6 + p_{k+1}[6:12]) + psi - dv
+//   fwd   x_{k+1} = A x_k - [0; KZ x_k + n6'_k]                     (serial, lanes 0-11)
+//   post  q2 = Z x_k + v6 + p_{k+1}[6:12] ; t = V q2 + rho ; y = -L^-T t
+// Stage-parallel levels are unrolled NT12 = ceil(12H/64) times with clamped task
+// indices so that every global load is unconditional and issued before any use;
+// the pre-pass data are fetched at entry, the post-pass data at the start of the
+// forward sweep (their L2 latency hides behind the serial recursion).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void riccati_solve(const DevParams& prm, const Smem& S, const double* __restrict__ gs, int lane) {
-    const int H = prm.H;
-    const double dt = prm.dt;
-    // pre 1: rho = L^-1 rr
-    for (int e = lane; e < 12 * H; e += 64) {
-        const int k = e / 12, r = e % 12;
-        const double* Li = gs + k * GS + GO_LINV + pk(r, 0);
-        const ldouble* rr = S.st + k * SK + SO_RRV;
+template <int NT12>
+__device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdouble* __restrict__ gs, const int H,
+                                                        const double dt, const int lane) {
+    constexpr int NT6 = (NT12 + 1) / 2;
+    const int n12 = 12 * H, n6 = 6 * H;
+    SUB_DECL
+    int k12[NT12], r12[NT12];
+    bool v12[NT12];
+#pragma unroll
+    for (int i = 0; i < NT12; ++i) {
+        const int e = lane + 64 * i;
+        v12[i] = e < n12;
+        const int ec = v12[i] ? e : n12 - 1;
+        k12[i] = ec / 12;
+        r12[i] = ec - 12 * k12[i];
+    }
+    int k6[NT6], m6[NT6];
+    bool v6[NT6];
+#pragma unroll
+    for (int i = 0; i < NT6; ++i) {
+        const int e = lane + 64 * i;
+        v6[i] = e < n6;
+        const int ec = v6[i] ? e : n6 - 1;
+        k6[i] = ec / 6;
+        m6[i] = ec - 6 * k6[i];
+    }
+    // ---- prefetch: L^-1 rows, V columns, Z columns ----
+    double li[NT12][12], zc[NT12][6], vc[NT6][12];
+#pragma unroll
+    for (int i = 0; i < NT12; ++i) {
+        const gdouble* Li = gs + k12[i] * GS + GO_LINV + pk(r12[i], 0);  // pk(r, c) < 78 for every c < 12
+        const gdouble* Z = gs + k12[i] * GS + GO_Z + r12[i];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) li[i][c] = Li[c];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) zc[i][m] = Z[m * 12];
+    }
+#pragma unroll
+    for (int i = 0; i < NT6; ++i) {
+        const gdouble* V = gs + k6[i] * GS + GO_V + m6[i] * 12;
+#pragma unroll
+        for (int r = 0; r < 12; ++r) vc[i][r] = V[r];
+    }
+    // pre 1: rho = L^-1 rr (masked arithmetic on unconditional loads)
+#pragma unroll
+    for (int i = 0; i < NT12; ++i) {
+        const ldouble* rr = S.st + k12[i] * SK + SO_RRV;
         double v = 0.0;
-        for (int c = 0; c <= r; ++c) v += Li[c] * rr[c];
-        S.st[k * SK + SO_RHO + r] = v;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) v += ((c <= r12[i]) ? li[i][c] : 0.0) * rr[c];
+        if (v12[i]) S.st[k12[i] * SK + SO_RHO + r12[i]] = v;
     }
     LMPC_SYNC();
     // pre 2: psi = V' rho
-    for (int e = lane; e < 6 * H; e += 64) {
-        const int k = e / 6, m = e % 6;
-        const double* V = gs + k * GS + GO_V;
-        const ldouble* rho = S.st + k * SK + SO_RHO;
+#pragma unroll
+    for (int i = 0; i < NT6; ++i) {
+        const ldouble* rho = S.st + k6[i] * SK + SO_RHO;
         double v = 0.0;
 #pragma unroll
-        for (int r = 0; r < 12; ++r) v += V[r * 6 + m] * rho[r];
-        S.st[k * SK + SO_PSI + m] = v;
+        for (int r = 0; r < 12; ++r) v += vc[i][r] * rho[r];
+        if (v6[i]) S.st[k6[i] * SK + SO_PSI + m6[i]] = v;
     }
     LMPC_SYNC();
-    // pre 3: cst_k = q_k - A_k' P2' psi   (k >= 1)
-    for (int e = lane; e < 12 * H; e += 64) {
-        const int k = e / 12, r = e % 12;
-        if (k == 0) continue;
-        const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-        const double* P2 = gs + k * GS + GO_P2;
-        const ldouble* psi = S.st + k * SK + SO_PSI;
-        double w[12];
+    // pre 3: cst'_k = -q x_ref,k-1 - Z'psi + (A'v)[r] - sum_m KZ[m][r] v[6+m]   (k >= 1)
 #pragma unroll
-        for (int c = 0; c < 12; ++c) {
-            double v = 0.0;
-#pragma unroll
-            for (int m = 0; m < 6; ++m) v += P2[m * 12 + c] * psi[m];
-            w[c] = v;
-        }
-        S.st[k * SK + SO_CST + r] = -prm.q[r] * S.xr[(k - 1) * 12 + r] - Atw_el(w, r, ck, sk, dt);
-    }
-    if (lane < 12) S.pa[lane] = -prm.q[lane] * S.xr[(H - 1) * 12 + lane];
-    LMPC_SYNC();
-    // backward: s = v_k + p_{k+1};  p_k = A's - (KZ)' s2 + cst_k
-    ldouble* pcur = S.pa;
-    ldouble* pnxt = S.pb;
-    for (int k = H - 1; k >= 0; --k) {
+    for (int i = 0; i < NT12; ++i) {
+        const int k = k12[i], r = r12[i];
         const ldouble* sl = S.st + k * SK;
-        if (lane < 12 && k > 0) {
-            const int r = lane;
-            const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-            double sv[12];
+        const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
+        double v = -S.qw[r] * S.xr[(k > 0 ? k - 1 : 0) * 12 + r] + Atw_el(sl + SO_VV, r, ck, sk, dt);
 #pragma unroll
-            for (int i = 0; i < 12; ++i) sv[i] = sl[SO_VV + i] + pcur[i];
-            double v = Atw_el(sv, r, ck, sk, dt);
-#pragma unroll
-            for (int m = 0; m < 6; ++m) v -= sl[SO_KZ + m * 12 + r] * sv[6 + m];
-            pnxt[r] = v + sl[SO_CST + r];
-        } else if (lane >= 16 && lane < 22) {
-            const int m = lane - 16;
-            S.st[k * SK + SO_S2 + m] = sl[SO_VV + 6 + m] + pcur[6 + m];
-        }
-        LMPC_SYNC();
-        ldouble* t = pcur;
-        pcur = pnxt;
-        pnxt = t;
+        for (int m = 0; m < 6; ++m) v -= zc[i][m] * sl[SO_PSI + m] + sl[SO_KZ + m * 12 + r] * sl[SO_VV + 6 + m];
+        if (v12[i] && k > 0) S.st[k * SK + SO_CST + r] = v;
     }
-    // n6 = K s2 + psi
-    for (int e = lane; e < 6 * H; e += 64) {
-        const int k = e / 6, m = e % 6;
-        const double* Kp = gs + k * GS + GO_K;
-        const ldouble* s2 = S.st + k * SK + SO_S2;
-        double v = S.st[k * SK + SO_PSI + m];
+    if (lane < 12) S.st[(H - 1) * SK + SO_PN + lane] = -S.qw[lane] * S.xr[(H - 1) * 12 + lane];
+    double kk[NT6][6];
 #pragma unroll
-        for (int n = 0; n < 6; ++n) v += Kp[m >= n ? pk(m, n) : pk(n, m)] * s2[n];
-        S.st[k * SK + SO_N6 + m] = v;
+    for (int i = 0; i < NT6; ++i) {
+        const gdouble* Kp = gs + k6[i] * GS + GO_K + m6[i] * 6;
+#pragma unroll
+        for (int n = 0; n < 6; ++n) kk[i][n] = Kp[n];
+    }
+    LMPC_SYNC();
+    SUB(0);
+    // ---- backward: p_k (into stage k-1's PN slot) ----
+    {
+        const int r = lane < 12 ? lane : 0;
+        const int ib = (r >= 9) ? 3 : 0;
+        const bool act = lane < 12;
+        for (int k = H - 1; k >= 1; --k) {
+            const ldouble* sl = S.st + k * SK;
+            const ldouble* p = sl + SO_PN;
+            const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
+            double w[3];
+            Mcol(ck, sk, r - 6, w);
+            if (r >= 9) {
+                w[0] = (r == 9) ? 1.0 : 0.0;
+                w[1] = (r == 10) ? 1.0 : 0.0;
+                w[2] = (r == 11) ? 1.0 : 0.0;
+            } else if (r < 6) {
+                w[0] = w[1] = w[2] = 0.0;
+            }
+            const double a0 = p[r] + sl[SO_CST + r];
+            const double a1 = w[0] * p[ib] + w[1] * p[ib + 1] + w[2] * p[ib + 2];
+            const double b0 = sl[SO_KZ + 0 * 12 + r] * p[6] + sl[SO_KZ + 1 * 12 + r] * p[7] + sl[SO_KZ + 2 * 12 + r] * p[8];
+            const double b1 = sl[SO_KZ + 3 * 12 + r] * p[9] + sl[SO_KZ + 4 * 12 + r] * p[10] + sl[SO_KZ + 5 * 12 + r] * p[11];
+            if (act) S.st[(k - 1) * SK + SO_PN + r] = a0 + dt * a1 - (b0 + b1);
+            LMPC_SYNC();
+        }
+    }
+    SUB(1);
+    // mid: n6'_k = K (v6 + p6) + psi - dv
+#pragma unroll
+    for (int i = 0; i < NT6; ++i) {
+        const ldouble* sl = S.st + k6[i] * SK;
+        double v = sl[SO_PSI + m6[i]] - sl[SO_DV + m6[i]];
+#pragma unroll
+        for (int n = 0; n < 6; ++n) v += kk[i][n] * (sl[SO_VV + 6 + n] + sl[SO_PN + 6 + n]);
+        if (v6[i]) S.st[k6[i] * SK + SO_N6 + m6[i]] = v;
     }
     if (lane < 12) S.st[SO_XS + lane] = S.hdr[lane];
+    // prefetch post-pass data (consumed after the forward sweep)
+    double zr[NT6][12], vr[NT12][6], lc[NT12][12];
+#pragma unroll
+    for (int i = 0; i < NT6; ++i) {
+        const gdouble* Z = gs + k6[i] * GS + GO_Z + m6[i] * 12;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) zr[i][c] = Z[c];
+    }
+#pragma unroll
+    for (int i = 0; i < NT12; ++i) {
+        const gdouble* V = gs + k12[i] * GS + GO_V + r12[i];
+        const gdouble* Li = gs + k12[i] * GS + GO_LINV;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) vr[i][m] = V[m * 12];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) lc[i][r] = Li[pk(r, r12[i])];  // in range for every r < 12; masked below
+    }
     LMPC_SYNC();
-    // forward: x_{k+1} = A x - [0; KZ x + n6 - dv]
-    for (int k = 0; k < H; ++k) {
-        const ldouble* sl = S.st + k * SK;
-        ldouble* xo = (k + 1 < H) ? S.st + (k + 1) * SK + SO_XS : S.xH;
-        if (lane < 12) {
-            const int r = lane;
+    SUB(2);
+    // ---- forward: x_{k+1} = A x - [0; KZ x + n6'] ----
+    {
+        const int r = lane < 12 ? lane : 0;
+        const bool act = lane < 12;
+        // (A x)[r] = x[r] + dt sum_j wa[j] x[ia+j]: rows 0-2 M[r][:] on x[6:9], rows 3-5 e_{r-3} on x[9:12]
+        const int ia = (r < 3) ? 6 : 9;
+        const int rk = (r >= 6) ? r - 6 : 0;
+        const double kzm = (r >= 6) ? 1.0 : 0.0;
+        for (int k = 0; k < H; ++k) {
+            const ldouble* sl = S.st + k * SK;
             const ldouble* x = sl + SO_XS;
+            ldouble* xo = (k + 1 < H) ? S.st + (k + 1) * SK + SO_XS : S.xH;
             const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-            double v = Ax_el(x, r, ck, sk, dt);
-            if (r >= 6) {
-                double kz = 0.0;
-#pragma unroll
-                for (int c = 0; c < 12; ++c) kz += sl[SO_KZ + (r - 6) * 12 + c] * x[c];
-                v += -kz - sl[SO_N6 + r - 6] + sl[SO_DV + r - 6];
-            }
-            xo[r] = v;
+            double wa[3];
+            wa[0] = (r == 0) ? ck : (r == 1) ? -sk : (r == 3) ? 1.0 : 0.0;
+            wa[1] = (r == 0) ? sk : (r == 1) ? ck : (r == 4) ? 1.0 : 0.0;
+            wa[2] = (r == 2 || r == 5) ? 1.0 : 0.0;
+            const ldouble* kz = sl + SO_KZ + rk * 12;
+            const double a0 = x[r] + dt * (wa[0] * x[ia] + wa[1] * x[ia + 1] + wa[2] * x[ia + 2]);
+            const double b0 = kz[0] * x[0] + kz[1] * x[1] + kz[2] * x[2] + kz[3] * x[3];
+            const double b1 = kz[4] * x[4] + kz[5] * x[5] + kz[6] * x[6] + kz[7] * x[7];
+            const double b2 = kz[8] * x[8] + kz[9] * x[9] + kz[10] * x[10] + kz[11] * x[11];
+            const double v = a0 - kzm * ((b0 + b1) + (b2 + sl[SO_N6 + rk]));
+            if (act) xo[r] = v;
+            LMPC_SYNC();
         }
-        LMPC_SYNC();
     }
-    // post 1: q2 = P2 (A x_k) + s2   -> SO_N6
-    for (int e = lane; e < 6 * H; e += 64) {
-        const int k = e / 6, m = e % 6;
-        const double* P2 = gs + k * GS + GO_P2;
-        const ldouble* x = S.st + k * SK + SO_XS;
-        const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-        double v = S.st[k * SK + SO_S2 + m];
+    SUB(3);
+    // post 1: q2 = Z x_k + v6 + p6   -> SO_N6
 #pragma unroll
-        for (int c = 0; c < 12; ++c) v += P2[m * 12 + c] * Ax_el(x, c, ck, sk, dt);
-        S.st[k * SK + SO_N6 + m] = v;
+    for (int i = 0; i < NT6; ++i) {
+        const ldouble* sl = S.st + k6[i] * SK;
+        double v = sl[SO_VV + 6 + m6[i]] + sl[SO_PN + 6 + m6[i]];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) v += zr[i][c] * sl[SO_XS + c];
+        if (v6[i]) S.st[k6[i] * SK + SO_N6 + m6[i]] = v;
     }
     LMPC_SYNC();
-    // post 2: t = V q2 + rho  -> SO_RHO
-    for (int e = lane; e < 12 * H; e += 64) {
-        const int k = e / 12, r = e % 12;
-        const double* V = gs + k * GS + GO_V;
-        double v = S.st[k * SK + SO_RHO + r];
+    // post 2: t = V q2 + rho  -> SO_RHO (in place: each entry is read by its own task only)
 #pragma unroll
-        for (int m = 0; m < 6; ++m) v += V[r * 6 + m] * S.st[k * SK + SO_N6 + m];
-        S.st[k * SK + SO_RHO + r] = v;
+    for (int i = 0; i < NT12; ++i) {
+        const ldouble* sl = S.st + k12[i] * SK;
+        double v = sl[SO_RHO + r12[i]];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) v += vr[i][m] * sl[SO_N6 + m];
+        if (v12[i]) S.st[k12[i] * SK + SO_RHO + r12[i]] = v;
     }
     LMPC_SYNC();
     // post 3: y = -L^-T t  -> SO_RRV
-    for (int e = lane; e < 12 * H; e += 64) {
-        const int k = e / 12, c = e % 12;
-        const double* Li = gs + k * GS + GO_LINV;
-        const ldouble* t = S.st + k * SK + SO_RHO;
+#pragma unroll
+    for (int i = 0; i < NT12; ++i) {
+        const ldouble* t = S.st + k12[i] * SK + SO_RHO;
         double v = 0.0;
-        for (int r = c; r < 12; ++r) v += Li[pk(r, c)] * t[r];
-        S.st[k * SK + SO_RRV + c] = -v;
+#pragma unroll
+        for (int r = 0; r < 12; ++r) v += ((r >= r12[i]) ? lc[i][r] : 0.0) * t[r];
+        if (v12[i]) S.st[k12[i] * SK + SO_RRV + r12[i]] = -v;
     }
     LMPC_SYNC();
+    SUB(4);
 }
 
 // Adjoint: lambda_{k+1} for every stage (SO_LAM) from the trajectory in SO_XS / xH.
@@ -779,6 +928,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         }
         S.G0[e] = v;
     }
+    if (lane < 12) S.qw[lane] = prm.q[lane];
     LMPC_SYNC();
 
     // ---- leg-step ownership and IPM state ----
@@ -898,9 +1048,16 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
             leg_rhs<LS>(S, valid, lsk, lsj, Rt, rt, T, up);
             LMPC_SYNC();
             STAMP(1);  // leg-step work (IPM/polish bookkeeping, stage prep)
-            if (mode != CORR) riccati_factor(prm, S, gs, lane);
+            if (mode != CORR) riccati_factor(S, (gdouble*)gs, H, dt, lane);
             STAMP(2);  // factorisation
-            riccati_solve(prm, S, gs, lane);
+            switch ((12 * H + 63) / 64) {
+                case 1: riccati_solve<1>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 2: riccati_solve<2>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 3: riccati_solve<3>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 4: riccati_solve<4>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 5: riccati_solve<5>(S, (const gdouble*)gs, H, dt, lane); break;
+                default: riccati_solve<6>(S, (const gdouble*)gs, H, dt, lane); break;
+            }
             STAMP(3);  // vector pass
             leg_u<LS>(S, valid, lsk, lsj, T, up, u);
             if (mode == PRED) {
@@ -1132,6 +1289,10 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
 }
 
 #ifdef LMPC_STAMPS
+extern "C" int lmpc_debug_substamps(unsigned long long* out, int nqp) {
+    if (nqp > STAMP_QPS) nqp = STAMP_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_substamps), (size_t)nqp * 16 * sizeof(unsigned long long)) == hipSuccess ? nqp : -1;
+}
 extern "C" int lmpc_debug_stamps(unsigned long long* out, int nqp) {
     if (nqp > STAMP_QPS) nqp = STAMP_QPS;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_stamps), (size_t)nqp * 8 * sizeof(unsigned long long)) == hipSuccess ? nqp : -1;

@@ -23,3 +23,20 @@ tot = buf[:n, :6].sum(1).astype(float)
 print(f"config {cid} H={H} B={count}: mean cycles/QP {tot.mean():.0f}  ipm_it {np.mean(it & 0xffff):.2f} rounds {np.mean(it >> 16):.2f}")
 for i, nm in enumerate(names):
     print(f"  {nm:9s} {buf[:n, i].astype(float).mean():12.0f}  ({100 * buf[:n, i].astype(float).mean() / tot.mean():5.1f}%)")
+
+# sub-phase stamps (accumulated over every launch above: 2 runs)
+L.lmpc_debug_substamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+sb = np.zeros((min(count, 4096), 16), dtype=np.uint64)
+n = L.lmpc_debug_substamps(sb.ctypes.data, sb.shape[0])
+sb = sb[:n].astype(float) / 2.0
+ipm = (it[:n] & 0xffff).astype(float)
+rnd = (it[:n] >> 16).astype(float)
+nfac = ipm + rnd  # one factorisation per IPM iteration (+ the final check) and per polish round (approx.)
+nsol = 2 * ipm + rnd
+sub = {0: "solve:pre", 1: "solve:backward", 2: "solve:mid", 3: "solve:forward", 4: "solve:post",
+       5: "factor:A", 6: "factor:B", 7: "factor:elim+out", 8: "factor:D(K)", 9: "factor:E(KZ)", 10: "factor:F(P)"}
+print(f"sub-phases (cycles per QP, per call; H={H})")
+for i, nm in sub.items():
+    per_qp = sb[:, i].mean()
+    calls = (nsol if i < 5 else nfac).mean()
+    print(f"  {nm:16s} {per_qp:12.0f}  per call {per_qp / calls:9.0f}  per stage {per_qp / calls / H:8.0f}")
