@@ -42,7 +42,17 @@
 
 namespace lmpc {
 
-#define LMPC_SYNC() __syncthreads()
+// One workgroup = one wavefront (blockDim 64, __launch_bounds__(64)): cross-lane exchange through LDS
+// needs only wavefront-scope ordering -- LDS operations of one wave are performed in order -- so the
+// "barrier" is a release/acquire fence pair at wavefront scope around a code-motion barrier.  Unlike
+// __syncthreads() it emits no s_waitcnt lgkmcnt(0): loads issued ahead (prefetches) stay in flight.
+constexpr int LMPC_WAVE = 64;
+#define LMPC_SYNC()                                              \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+    } while (0)
 
 // Diagnostic build only (-DLMPC_STAMPS): per-phase cycle counters of QP 0..STAMP_QPS-1,
 // written to a buffer no other code reads.  Never compiled into the product library.
@@ -138,16 +148,16 @@ constexpr int SO_RR = 0;     // 4 x 3x3 input Hessian blocks T'RtT
 constexpr int SO_BT = 36;    // 6 x 12 Bt = G0 T
 constexpr int SO_DV = 108;   // 6   d_k[6:12] = G0 up - g dt e5
 constexpr int SO_RRV = 114;  // 12  input linear term rr (later: y)
-constexpr int SO_KZ = 126;   // 6 x 12 K Z
-constexpr int SO_VV = 198;   // 12  v = P_{k+1} d_k
-constexpr int SO_CST = 210;  // 12  q_k - Z' psi
-constexpr int SO_PSI = 222;  // 6   V' L^-1 rr
-constexpr int SO_RHO = 228;  // 12  L^-1 rr (later: t)
-constexpr int SO_N6 = 240;   // 6   K s2 + psi - dv (later: q2)
-constexpr int SO_PN = 246;   // 12  p_{k+1}
-constexpr int SO_XS = 258;   // 12  x_k
-constexpr int SO_LAM = 270;  // 12  lambda_{k+1}
-constexpr int SK = 282;
+constexpr int SO_N = 126;    // 12 x 12 closed-loop N_k = A_k - [0; K Z]
+constexpr int SO_VV = 270;   // 12  v = P_{k+1} d_k
+constexpr int SO_CST = 282;  // 12  q_k - Z' psi + N' v
+constexpr int SO_PSI = 294;  // 6   V' L^-1 rr
+constexpr int SO_RHO = 300;  // 12  L^-1 rr (later: t)
+constexpr int SO_N6 = 312;   // 6   K s2 + psi - dv (later: q2)
+constexpr int SO_PN = 318;   // 12  p_{k+1}
+constexpr int SO_XS = 330;   // 12  x_k
+constexpr int SO_LAM = 342;  // 12  lambda_{k+1}
+constexpr int SK = 354;
 // global scratch per stage
 constexpr int GO_LINV = 0;   // 78 packed L^-1 (lower, row-packed)
 constexpr int GO_V = 78;     // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
@@ -169,6 +179,7 @@ struct Smem {
     ldouble* PNL;  // 72   pivot block columns (3 columns x 12 rows), double-buffered
     ldouble* VL;   // 72   V = L^-1 Bt', column-major
     ldouble* K;    // 36
+    ldouble* KZ;   // 72   K Z of the current stage
     ldouble* pa;   // 12
     ldouble* pb;   // 12
     ldouble* qw;   // 12  state weights q
@@ -176,7 +187,7 @@ struct Smem {
 };
 
 // fixed-size LDS members, in carve order; the total must equal LDS_FIXED_DOUBLES (lmpc_device.h)
-constexpr int LDS_SIZES[] = {72, 40, 12, 144, 144, 72, 72, 144, 72, 72, 36, 12, 12, 12};
+constexpr int LDS_SIZES[] = {72, 40, 12, 144, 144, 72, 72, 144, 72, 72, 36, 72, 12, 12, 12};
 constexpr int lds_fixed_sum() {
     int t = 0;
     for (int v : LDS_SIZES) t += v;
@@ -184,6 +195,7 @@ constexpr int lds_fixed_sum() {
 }
 static_assert(lds_fixed_sum() == LDS_FIXED_DOUBLES, "LDS carve and lds_doubles() disagree");
 static_assert(SK == LDS_STAGE_DOUBLES, "per-stage LDS slot and lds_doubles() disagree");
+static_assert(GS == SCRATCH_STAGE_DOUBLES, "per-stage global scratch and scratch_doubles_per_qp() disagree");
 
 __device__ __forceinline__ Smem carve(double* sm, int H) {
     Smem s;
@@ -199,6 +211,7 @@ __device__ __forceinline__ Smem carve(double* sm, int H) {
     s.PNL = p; p += 72;
     s.VL = p; p += 72;
     s.K = p; p += 36;
+    s.KZ = p; p += 72;
     s.pa = p; p += 12;
     s.pb = p; p += 12;
     s.qw = p; p += 12;
@@ -215,6 +228,14 @@ __device__ __forceinline__ double rsq_nr(double x) {
     const double h = 0.5 * x;
     y = y * fma(-h * y, y, 1.5);
     y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+// 1/x to full fp64 precision: hardware estimate + two Newton steps
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    y = fma(y, fma(-x, y, 1.0), y);
     return y;
 }
 
@@ -400,7 +421,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         }
         LMPC_SYNC();
         SUB(8);
-        // ---- level E: KZ = K Z ----
+        // ---- level E: KZ = K Z ; closed-loop N_k = A_k - [0; KZ] into the stage slot ----
         if (lane < 24) {
             const bool lo = qg < 2;
             const ldouble* zb = lo ? P + 72 + 3 * qg : S.PA6 + 36 + 3 * (qg - 2);
@@ -413,7 +434,23 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
                 double v = 0.0;
 #pragma unroll
                 for (int n = 0; n < 6; ++n) v += kk[n] * zb[n * zs + i];
-                sl[SO_KZ + qr * 12 + 3 * qg + i] = v;
+                S.KZ[qr * 12 + 3 * qg + i] = v;
+                sl[SO_N + (6 + qr) * 12 + 3 * qg + i] = ((6 + qr == 3 * qg + i) ? 1.0 : 0.0) - v;
+            }
+        } else if (lane < 48) {
+            // rows 0-5 of A_k: [I  0  dt M(yaw)  0 ; 0  I  0  dt I]
+            const int ra = (lane - 24) >> 2, cg = (lane - 24) & 3;
+            double mrow[3];  // row ra of M (rows 0-2 only)
+            mrow[0] = (ra == 0) ? ck : (ra == 1) ? -sk : 0.0;
+            mrow[1] = (ra == 0) ? sk : (ra == 1) ? ck : 0.0;
+            mrow[2] = (ra == 2) ? 1.0 : 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int c = 3 * cg + i;
+                double v = (ra == c) ? 1.0 : 0.0;
+                if (ra < 3 && cg == 2) v += dt * mrow[i];
+                if (ra >= 3 && cg == 3 && c == ra + 6) v += dt;
+                sl[SO_N + ra * 12 + c] = v;
             }
         }
         LMPC_SYNC();
@@ -455,7 +492,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
                     const double corr = cb[i] * wr[0] + cb[6 + i] * wr[1] + cb[12 + i] * wr[2];
                     v += br ? dt * corr : 0.0;
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) v -= zc[m] * sl[SO_KZ + m * 12 + 3 * qg + i];
+                    for (int m = 0; m < 6; ++m) v -= zc[m] * S.KZ[m * 12 + 3 * qg + i];
                     Pn[qr * 12 + 3 * qg + i] = v;
                 }
             }
@@ -470,10 +507,10 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 
 // ---------------------------------------------------------------------------
 // Vector pass.  Reads rr (SO_RRV) per stage; leaves y in SO_RRV and x_k in SO_XS / xH.
-//   pre   rho = L^-1 rr ; psi = V' rho ; cst'_k = q_k - Z'psi + A'v - (KZ)'v6
-//   back  p_k = A'p_{k+1} - (KZ)' p_{k+1}[6:12] + cst'_k          (serial, lanes 0-11)
+//   pre   rho = L^-1 rr ; psi = V' rho ; cst'_k = q_k - Z'psi + N_k' v
+//   back  p_k = N_k' p_{k+1} + cst'_k,  N_k = A_k - [0; KZ_k]       (serial, lanes 0-11)
 //   mid   n6'_k = K (v6 + p_{k+1}[6:12]) + psi - dv
-//   fwd   x_{k+1} = A x_k - [0; KZ x_k + n6'_k]                     (serial, lanes 0-11)
+//   fwd   x_{k+1} = N_k x_k - [0; n6'_k]                              (serial, lanes 0-11)
 //   post  q2 = Z x_k + v6 + p_{k+1}[6:12] ; t = V q2 + rho ; y = -L^-T t
 // Stage-parallel levels are unrolled NT12 = ceil(12H/64) times with clamped task
 // indices so that every global load is unconditional and issued before any use;
@@ -543,15 +580,16 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
         if (v6[i]) S.st[k6[i] * SK + SO_PSI + m6[i]] = v;
     }
     LMPC_SYNC();
-    // pre 3: cst'_k = -q x_ref,k-1 - Z'psi + (A'v)[r] - sum_m KZ[m][r] v[6+m]   (k >= 1)
+    // pre 3: cst'_k = -q x_ref,k-1 - Z'psi + N_k' v   (k >= 1)
 #pragma unroll
     for (int i = 0; i < NT12; ++i) {
         const int k = k12[i], r = r12[i];
         const ldouble* sl = S.st + k * SK;
-        const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-        double v = -S.qw[r] * S.xr[(k > 0 ? k - 1 : 0) * 12 + r] + Atw_el(sl + SO_VV, r, ck, sk, dt);
+        double v = -S.qw[r] * S.xr[(k > 0 ? k - 1 : 0) * 12 + r];
 #pragma unroll
-        for (int m = 0; m < 6; ++m) v -= zc[i][m] * sl[SO_PSI + m] + sl[SO_KZ + m * 12 + r] * sl[SO_VV + 6 + m];
+        for (int m = 0; m < 6; ++m) v -= zc[i][m] * sl[SO_PSI + m];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) v += sl[SO_N + j * 12 + r] * sl[SO_VV + j];
         if (v12[i] && k > 0) S.st[k * SK + SO_CST + r] = v;
     }
     if (lane < 12) S.st[(H - 1) * SK + SO_PN + lane] = -S.qw[lane] * S.xr[(H - 1) * 12 + lane];
@@ -564,29 +602,33 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
     }
     LMPC_SYNC();
     SUB(0);
-    // ---- backward: p_k (into stage k-1's PN slot) ----
+    // ---- backward: p_k = N_k' p_{k+1} + cst'_k (into stage k-1's PN slot); column r of N_k is
+    // fetched one step ahead so only the broadcast reads of p_{k+1} sit on the critical path ----
     {
         const int r = lane < 12 ? lane : 0;
-        const int ib = (r >= 9) ? 3 : 0;
         const bool act = lane < 12;
+        double nc[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) nc[j] = S.st[(H - 1) * SK + SO_N + j * 12 + r];
         for (int k = H - 1; k >= 1; --k) {
             const ldouble* sl = S.st + k * SK;
-            const ldouble* p = sl + SO_PN;
-            const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-            double w[3];
-            Mcol(ck, sk, r - 6, w);
-            if (r >= 9) {
-                w[0] = (r == 9) ? 1.0 : 0.0;
-                w[1] = (r == 10) ? 1.0 : 0.0;
-                w[2] = (r == 11) ? 1.0 : 0.0;
-            } else if (r < 6) {
-                w[0] = w[1] = w[2] = 0.0;
-            }
-            const double a0 = p[r] + sl[SO_CST + r];
-            const double a1 = w[0] * p[ib] + w[1] * p[ib + 1] + w[2] * p[ib + 2];
-            const double b0 = sl[SO_KZ + 0 * 12 + r] * p[6] + sl[SO_KZ + 1 * 12 + r] * p[7] + sl[SO_KZ + 2 * 12 + r] * p[8];
-            const double b1 = sl[SO_KZ + 3 * 12 + r] * p[9] + sl[SO_KZ + 4 * 12 + r] * p[10] + sl[SO_KZ + 5 * 12 + r] * p[11];
-            if (act) S.st[(k - 1) * SK + SO_PN + r] = a0 + dt * a1 - (b0 + b1);
+            // the reads this step waits for are issued first (LDS returns in order), the prefetch after
+            double pv[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) pv[j] = sl[SO_PN + j];
+            const double cst = sl[SO_CST + r];
+            double nn[12];
+            const ldouble* nxt = S.st + (k > 1 ? k - 1 : 1) * SK + SO_N + r;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) nn[j] = nxt[j * 12];
+            const double a0 = cst + nc[0] * pv[0] + nc[1] * pv[1] + nc[2] * pv[2] + nc[3] * pv[3];
+            const double a1 = nc[4] * pv[4] + nc[5] * pv[5] + nc[6] * pv[6] + nc[7] * pv[7];
+            const double a2 = nc[8] * pv[8] + nc[9] * pv[9] + nc[10] * pv[10] + nc[11] * pv[11];
+            // branch-free: idle lanes write a dummy word (a branch would sink the reads behind the prefetch)
+            ldouble* dst = act ? S.st + (k - 1) * SK + SO_PN + r : S.pa;
+            *dst = a0 + (a1 + a2);
+#pragma unroll
+            for (int j = 0; j < 12; ++j) nc[j] = nn[j];
             LMPC_SYNC();
         }
     }
@@ -601,7 +643,40 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
         if (v6[i]) S.st[k6[i] * SK + SO_N6 + m6[i]] = v;
     }
     if (lane < 12) S.st[SO_XS + lane] = S.hdr[lane];
-    // prefetch post-pass data (consumed after the forward sweep)
+    LMPC_SYNC();
+    SUB(2);
+    // ---- forward: x_{k+1} = N_k x_k - [0; n6'_k]; row r of N_{k+1} is fetched one step ahead ----
+    {
+        const int r = lane < 12 ? lane : 0;
+        const bool act = lane < 12;
+        const int r6 = (r >= 6) ? r - 6 : 0;
+        const double sel = (r >= 6) ? 1.0 : 0.0;
+        double nr[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) nr[j] = S.st[SO_N + r * 12 + j];
+        for (int k = 0; k < H; ++k) {
+            const ldouble* sl = S.st + k * SK;
+            ldouble* xo = (k + 1 < H) ? S.st + (k + 1) * SK + SO_XS : S.xH;
+            double x[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) x[j] = sl[SO_XS + j];
+            const double n6 = sl[SO_N6 + r6];
+            double nn[12];
+            const ldouble* nxt = S.st + (k + 1 < H ? k + 1 : k) * SK + SO_N + r * 12;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) nn[j] = nxt[j];
+            const double a0 = nr[0] * x[0] + nr[1] * x[1] + nr[2] * x[2] + nr[3] * x[3] - sel * n6;
+            const double a1 = nr[4] * x[4] + nr[5] * x[5] + nr[6] * x[6] + nr[7] * x[7];
+            const double a2 = nr[8] * x[8] + nr[9] * x[9] + nr[10] * x[10] + nr[11] * x[11];
+            ldouble* dst = act ? xo + r : S.pa;
+            *dst = a0 + (a1 + a2);
+#pragma unroll
+            for (int j = 0; j < 12; ++j) nr[j] = nn[j];
+            LMPC_SYNC();
+        }
+    }
+    SUB(3);
+    // post-pass data (fetched after the forward sweep: holding it across the serial loop starves it of registers)
     double zr[NT6][12], vr[NT12][6], lc[NT12][12];
 #pragma unroll
     for (int i = 0; i < NT6; ++i) {
@@ -618,36 +693,6 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
         for (int r = 0; r < 12; ++r) lc[i][r] = Li[pk(r, r12[i])];  // in range for every r < 12; masked below
     }
-    LMPC_SYNC();
-    SUB(2);
-    // ---- forward: x_{k+1} = A x - [0; KZ x + n6'] ----
-    {
-        const int r = lane < 12 ? lane : 0;
-        const bool act = lane < 12;
-        // (A x)[r] = x[r] + dt sum_j wa[j] x[ia+j]: rows 0-2 M[r][:] on x[6:9], rows 3-5 e_{r-3} on x[9:12]
-        const int ia = (r < 3) ? 6 : 9;
-        const int rk = (r >= 6) ? r - 6 : 0;
-        const double kzm = (r >= 6) ? 1.0 : 0.0;
-        for (int k = 0; k < H; ++k) {
-            const ldouble* sl = S.st + k * SK;
-            const ldouble* x = sl + SO_XS;
-            ldouble* xo = (k + 1 < H) ? S.st + (k + 1) * SK + SO_XS : S.xH;
-            const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-            double wa[3];
-            wa[0] = (r == 0) ? ck : (r == 1) ? -sk : (r == 3) ? 1.0 : 0.0;
-            wa[1] = (r == 0) ? sk : (r == 1) ? ck : (r == 4) ? 1.0 : 0.0;
-            wa[2] = (r == 2 || r == 5) ? 1.0 : 0.0;
-            const ldouble* kz = sl + SO_KZ + rk * 12;
-            const double a0 = x[r] + dt * (wa[0] * x[ia] + wa[1] * x[ia + 1] + wa[2] * x[ia + 2]);
-            const double b0 = kz[0] * x[0] + kz[1] * x[1] + kz[2] * x[2] + kz[3] * x[3];
-            const double b1 = kz[4] * x[4] + kz[5] * x[5] + kz[6] * x[6] + kz[7] * x[7];
-            const double b2 = kz[8] * x[8] + kz[9] * x[9] + kz[10] * x[10] + kz[11] * x[11];
-            const double v = a0 - kzm * ((b0 + b1) + (b2 + sl[SO_N6 + rk]));
-            if (act) xo[r] = v;
-            LMPC_SYNC();
-        }
-    }
-    SUB(3);
     // post 1: q2 = Z x_k + v6 + p6   -> SO_N6
 #pragma unroll
     for (int i = 0; i < NT6; ++i) {
@@ -765,6 +810,32 @@ __device__ bool leg_basis(int act, double mu, double fzmax, double T[9], double 
         for (int i = 0; i < 3; ++i) T[i * 3 + 0] = t[i] * in;
     }
     return false;
+}
+
+// Interior-point stage data: T = I (stance) / 0 (swing), up = 0, so Rr = Rt (identity for a swing
+// leg), Bt = G0_j masked by contact, dv = -g dt e5.
+template <int LS>
+__device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const Smem& S, const bool (&valid)[LS],
+                                                   const bool (&st)[LS], const int (&lsk)[LS], const int (&lsj)[LS],
+                                                   const double (&Rt)[LS][6]) {
+#pragma unroll
+    for (int t = 0; t < LS; ++t) {
+        if (!valid[t]) continue;
+        const int k = lsk[t], j = lsj[t];
+        ldouble* sl = S.st + k * SK;
+        const double on = st[t] ? 1.0 : 0.0, off = 1.0 - on;
+        const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
+#pragma unroll
+        for (int e = 0; e < 9; ++e) sl[SO_RR + j * 9 + e] = on * R3[e] + ((e % 4 == 0) ? off : 0.0);
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) sl[SO_BT + m * 12 + 3 * j + a] = on * S.G0[m * 12 + 3 * j + a];
+        if (j == 0) {
+#pragma unroll
+            for (int m = 0; m < 6; ++m) sl[SO_DV + m] = (m == 5) ? -prm.grav * prm.dt : 0.0;
+        }
+    }
 }
 
 // Per-leg-step stage data: Rr = T'RtT (fixed components -> identity), Bt = G0_j T, dv (quad-reduced).
@@ -971,7 +1042,11 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         int mode = PRED;
         int act[LS];
         bool apex[LS];
-        double dsa[LS][5], dza[LS][5];
+        double dsa[LS][5], dza[LS][5], is[LS][5];
+#pragma unroll
+        for (int t = 0; t < LS; ++t)
+#pragma unroll
+            for (int i = 0; i < 5; ++i) is[t][i] = 0.0;
         double mu_c = 0.0, smu = 0.0;
         for (;;) {
             if (mode == PRED) {
@@ -1004,7 +1079,8 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                         if (st[t]) {
 #pragma unroll
                             for (int i = 0; i < 5; ++i) {
-                                W[i] = z[t][i] / s[t][i];
+                                is[t][i] = rcp_nr(s[t][i]);  // 1/s, reused by the whole predictor-corrector step
+                                W[i] = z[t][i] * is[t][i];
                                 wv[i] = W[i] * (s[t][i] - (i == 4 ? fzmax : 0.0));
                             }
                         }
@@ -1044,7 +1120,8 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                     rt[t][0] = rt[t][1] = rt[t][2] = 0.0;
                 }
             }
-            if (mode != CORR) leg_stage_prep<LS>(prm, S, valid, lsk, lsj, Rt, T, up);
+            if (mode == PRED) leg_stage_prep_ipm<LS>(prm, S, valid, st, lsk, lsj, Rt);
+            else if (mode == POLISH) leg_stage_prep<LS>(prm, S, valid, lsk, lsj, Rt, T, up);
             leg_rhs<LS>(S, valid, lsk, lsj, Rt, rt, T, up);
             LMPC_SYNC();
             STAMP(1);  // leg-step work (IPM/polish bookkeeping, stage prep)
@@ -1072,9 +1149,10 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
 #pragma unroll
                     for (int i = 0; i < 5; ++i) {
                         dsa[t][i] = -o[i] - s[t][i];
-                        dza[t][i] = -z[t][i] - (z[t][i] / s[t][i]) * dsa[t][i];
-                        if (dsa[t][i] < 0.0) amax = fmin(amax, -s[t][i] / dsa[t][i]);
-                        if (dza[t][i] < 0.0) amax = fmin(amax, -z[t][i] / dza[t][i]);
+                        dza[t][i] = -z[t][i] - z[t][i] * is[t][i] * dsa[t][i];
+                        // fraction to the boundary: the hardware reciprocal estimate is ample here
+                        if (dsa[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(dsa[t][i]));
+                        if (dza[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dza[t][i]));
                     }
                 }
                 const double aa = wave_min(amax);
@@ -1093,8 +1171,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                     double wv[5];
 #pragma unroll
                     for (int i = 0; i < 5; ++i)
-                        wv[i] = (z[t][i] / s[t][i]) * (s[t][i] - (i == 4 ? fzmax : 0.0)) +
-                                (smu - dsa[t][i] * dza[t][i]) / s[t][i];
+                        wv[i] = (z[t][i] * (s[t][i] - (i == 4 ? fzmax : 0.0)) + smu - dsa[t][i] * dza[t][i]) * is[t][i];
                     cons_tw(wv, mu, rt[t]);
                 }
                 mode = CORR;
@@ -1111,9 +1188,9 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
 #pragma unroll
                     for (int i = 0; i < 5; ++i) {
                         ds[t][i] = -o[i] - s[t][i];
-                        dz[t][i] = (smu - z[t][i] * s[t][i] - dsa[t][i] * dza[t][i] - z[t][i] * ds[t][i]) / s[t][i];
-                        if (ds[t][i] < 0.0) amax = fmin(amax, -s[t][i] / ds[t][i]);
-                        if (dz[t][i] < 0.0) amax = fmin(amax, -z[t][i] / dz[t][i]);
+                        dz[t][i] = (smu - z[t][i] * s[t][i] - dsa[t][i] * dza[t][i] - z[t][i] * ds[t][i]) * is[t][i];
+                        if (ds[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(ds[t][i]));
+                        if (dz[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dz[t][i]));
                     }
                 }
                 const double alpha = fmin(1.0, 0.99 * wave_min(amax));
@@ -1275,7 +1352,7 @@ template __global__ void lmpc_qp_kernel<2>(const DevParams, const double*, const
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, int batch, double* grf,
                      int32_t* status, int32_t* iters, double* scratch, hipStream_t stream) {
     const size_t lds = lds_bytes(prm.H);
-    const dim3 grid(batch), block(64);
+    const dim3 grid(batch), block(LMPC_WAVE);  // LMPC_SYNC() relies on exactly one wavefront per workgroup
     if (4 * prm.H <= 64) {
         (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(lmpc_qp_kernel<1>, grid, block, lds, stream, prm, rec, contact, batch, grf, status, iters,
