@@ -58,13 +58,13 @@ def main():
 
     cfg = synth.CONFIGS[args.config]
     H = cfg["H"]
-    if args.batch is not None:
-        B = args.batch
-    elif args.config == 4:
-        B = cfg["batch"] // world
+    strong = args.batch is None and args.config == 4  # config 4: a fixed global batch split over the ranks
+    if strong:
+        first, last = D.split_range(rank, world, cfg["batch"])
+        B = last - first
     else:
-        B = cfg["batch"]
-    first, _ = D.shard_range(rank, world, B)
+        B = args.batch if args.batch is not None else cfg["batch"]
+        first, _ = D.shard_range(rank, world, B)
     p, H, rec, con = synth.config_batch(args.config, count=B, first_index=first)
 
     solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank)
@@ -103,7 +103,8 @@ def main():
     pol_mean = float(np.mean(it >> 16))
     flop_per_qp = roofline.qp_flop(H, ipm_mean, pol_mean)
     achieved_tf = flop_per_qp * B / (kernel_ms * 1e-3) / 1e12
-    total_qps = world * B * args.steps / t_max
+    global_batch = cfg["batch"] if strong else B * world
+    total_qps = global_batch * args.steps / t_max
 
     stats = D.sum_over_ranks([(st == 0).sum(), (st == 1).sum(), (st == 2).sum()], dist, dev)
 
@@ -143,7 +144,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (Philox-seeded perturbed states, SURVEY.md 8d)",
@@ -151,7 +152,7 @@ def main():
                 "workload": cfg["name"] if args.batch is None else f"{cfg['name']}@b{B}",
                 "horizon": H,
                 "batch_per_gpu": B,
-                "global_batch": B * world,
+                "global_batch": global_batch,
                 "robot": cfg["robot"],
                 "gait": "mixed" if cfg["gait"] < 0 else ["trot", "crawl", "trot_with_stand", "stand"][cfg["gait"]],
                 "parallelism": f"dp{world} (independent QP shards, no collective)",

@@ -30,7 +30,7 @@ constexpr int LDS_STAGE_DOUBLES = 354;  // per-stage slot (SK)
 inline int lds_doubles(int H) { return LDS_FIXED_DOUBLES + 14 * H + LDS_STAGE_DOUBLES * H; }
 inline size_t lds_bytes(int H) { return (size_t)lds_doubles(H) * sizeof(double); }
 // Global scratch (doubles) per QP: L^-1, V, K, Z per stage (GS in lmpc_kernels.hip, static_asserted).
-constexpr int SCRATCH_STAGE_DOUBLES = 258;
+constexpr int SCRATCH_STAGE_DOUBLES = 260;
 inline size_t scratch_doubles_per_qp(int H) { return (size_t)SCRATCH_STAGE_DOUBLES * H; }
 
 }  // namespace lmpc

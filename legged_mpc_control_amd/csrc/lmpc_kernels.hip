@@ -82,25 +82,42 @@ typedef __attribute__((address_space(3))) double ldouble;
 // Explicit global address space for the per-QP scratch (outlined functions would otherwise use flat ops).
 typedef __attribute__((address_space(1))) double gdouble;
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// ---- wave reductions without LDS: DPP inside 16-lane rows, readlane across the 4 rows ----
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+constexpr int DPP_QP_1032 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_QP_2301 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int DPP_ROR4 = 0x124;    // row_ror:4
+constexpr int DPP_ROR8 = 0x128;    // row_ror:8
+struct OpSum { __device__ static double f(double a, double b) { return a + b; } };
+struct OpMin { __device__ static double f(double a, double b) { return fmin(a, b); } };
+struct OpMax { __device__ static double f(double a, double b) { return fmax(a, b); } };
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v) {
+    v = Op::f(v, dpp_f64<DPP_QP_1032>(v));
+    v = Op::f(v, dpp_f64<DPP_QP_2301>(v));
+    v = Op::f(v, dpp_f64<DPP_ROR4>(v));
+    v = Op::f(v, dpp_f64<DPP_ROR8>(v));  // every lane holds its row's result
+    return Op::f(Op::f(readlane_f64(v, 0), readlane_f64(v, 16)), Op::f(readlane_f64(v, 32), readlane_f64(v, 48)));
 }
+__device__ __forceinline__ double wave_sum(double v) { return wave_reduce<OpSum>(v); }
+__device__ __forceinline__ double wave_min(double v) { return wave_reduce<OpMin>(v); }
+__device__ __forceinline__ double wave_max(double v) { return wave_reduce<OpMax>(v); }
 // sum over the 4 lanes of a stage (lanes 4q..4q+3 = legs of one stage)
 __device__ __forceinline__ double quad_sum(double v) {
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
+    v += dpp_f64<DPP_QP_1032>(v);
+    v += dpp_f64<DPP_QP_2301>(v);
     return v;
 }
 
@@ -163,7 +180,8 @@ constexpr int GO_LINV = 0;   // 78 packed L^-1 (lower, row-packed)
 constexpr int GO_V = 78;     // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
 constexpr int GO_K = 150;    // 6 x 6 K = V'V
 constexpr int GO_Z = 186;    // 6 x 12 Z = P2_{k+1} A_k
-constexpr int GS = 258;
+constexpr int GO_DUMMY = 258;  // sink for the branch-free masked stores
+constexpr int GS = 260;
 
 struct Smem {
     ldouble* G0;   // 72
@@ -221,13 +239,11 @@ __device__ __forceinline__ Smem carve(double* sm, int H) {
     return s;
 }
 
-// 1/sqrt(x) to full fp64 precision: hardware estimate + two Newton steps
-// (cheaper than the correctly-rounded sqrt + divide sequences).
+// 1/sqrt(x): hardware estimate + one Newton step (cheaper than the correctly-rounded sqrt + divide).
 __device__ __forceinline__ double rsq_nr(double x) {
+    // v_rsq_f64 is good to 2^-24 on gfx950 (tools/ubench/rsq_acc.hip); one Newton step -> ~4e-15
     double y = __builtin_amdgcn_rsq(x);
-    const double h = 0.5 * x;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-0.5 * x * y, y, 1.5);
     return y;
 }
 
@@ -266,96 +282,97 @@ __device__ __forceinline__ double Atw_el(Ptr w, int r, double ck, double sk, dou
 // ---------------------------------------------------------------------------
 // Riccati factorisation (backward, matrix part).
 //
-// Every lane has a fixed role per level (no task loops, no index decoding on
-// the critical path); 13 barriers per stage:
-//   A  C = P22 Bt (lanes 0-23) | PA6 = (P A)[:, 6:12] (24-47) | v = P d (48-59)
-//   B  Guu = blockdiag(Rr) + Bt' C, written column-major (lanes 0-47)
-//   elimination of [Guu | Bt' | I] by 3x3 leg blocks: lane j < 30 keeps column j
-//      in registers; per block: the pivot columns go to LDS, every lane factors
-//      the 3x3 pivot (rsq + Newton), lanes < 27 form the panel L_ba, every
-//      column lane applies it  -> V = L^-1 Bt' (lanes 12-17), L^-1 (lanes 18-29)
-//   D  K = V'V (lanes 0-35)
-//   E  KZ = K Z, Z = P2 A = [P2[:, 0:6] | PA6[6:12]] (lanes 0-23)
-//   F  P_k = Q + A'PA - Z'(KZ) into the other P buffer (lanes 0-47), with
-//      A'PA assembled from P and PA6 (A = I + dt N touches 6 columns / rows only)
+// The dense 12x12 products run on the fp64 matrix cores (v_mfma_f64_16x16x4f64,
+// 12x12 padded to 16x16).  Accumulator layout: lane l, register i holds row
+// (l>>4)+4i, column l&15 -- which is also the B operand of k-block i, and, for a
+// symmetric matrix, the A operand of k-block i.  So P_{k+1} stays in registers and
+// every product feeds the next without an LDS round trip:
+//   C^ = P B^            (B^ = [0; Bt | dv]: rows 6-11 hold Bt, column 12 dv -> v = P d)
+//   Guu = Rr + B^' C^     (the 12x12 input Hessian block plus the lifted state cost)
+//   PA = P A_k
+//   [block Cholesky of Guu with [Bt' | I] eliminated alongside, VALU, one column per lane]
+//   K^ = V^' V^           (V^ = [0 | V]: K lands in rows/columns 6-11, aligned with PA's rows)
+//   KZ^ = K^ PA           (rows 6-11 = K Z,  Z = P2 A = rows 6-11 of PA)
+//   P_k = Q + A'PA - PA' KZ^ ;  N_k = A_k - KZ^ (closed-loop matrix for the vector pass)
 // ---------------------------------------------------------------------------
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+// entry (r, c) of A_k = I + dt N(yaw) (zero padding outside 12x12)
+__device__ __forceinline__ double A_entry(int r, int c, double ck, double sk, double dt) {
+    if (r >= 12 || c >= 12) return 0.0;
+    double v = (r == c) ? 1.0 : 0.0;
+    if (r < 3 && c >= 6 && c < 9) {
+        const int j = c - 6;
+        const double m = (r == 0) ? ((j == 0) ? ck : (j == 1) ? sk : 0.0)
+                       : (r == 1) ? ((j == 0) ? -sk : (j == 1) ? ck : 0.0)
+                                  : ((j == 2) ? 1.0 : 0.0);
+        v += dt * m;
+    }
+    if (r >= 3 && r < 6 && c == r + 6) v += dt;
+    return v;
+}
+
 __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, const int H, const double dt,
                                                          const int lane) {
-    // lane-static roles
-    const int qr = lane >> 2, qg = lane & 3;              // row / 3-column group of a 12-wide output
-    const int tA = lane - 24, rA = tA >> 1, cgA = tA & 1;  // PA6 task (lanes 24-47)
-    const int dm = lane / 6, dn = lane - 6 * (lane / 6);   // K task (lanes 0-35)
-    const int qr3 = qr / 3, qrm3 = qr - 3 * (qr / 3);
-    const double qq = S.qw[qr < 12 ? qr : 0];
-    const double qdiag[3] = {(qr == 3 * qg) ? qq : 0.0, (qr == 3 * qg + 1) ? qq : 0.0, (qr == 3 * qg + 2) ? qq : 0.0};
-    ldouble* P = S.P;
-    ldouble* Pn = S.Pn;
-    for (int e = lane; e < 144; e += 64) P[e] = (e % 13 == 0) ? S.qw[e / 13] : 0.0;
-    LMPC_SYNC();
+    const int lc = lane & 15, lr = lane >> 4;  // accumulator layout: column lc, rows lr + 4i
+    d4 P;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        P[i] = (r == lc && r < 12) ? S.qw[r < 12 ? r : 0] : 0.0;
+    }
+    const d4 Qd = P;
     SUB_DECL
     for (int k = H - 1; k >= 0; --k) {
         const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
         ldouble* sl = S.st + k * SK;
         gdouble* g = gs + k * GS;
         const ldouble* Bt = sl + SO_BT;
-        // ---- level A ----
-        if (lane < 24) {
-            double p[6];
+        // ---- operands: A_k (k-blocks 0-2) and B^ (k-blocks 1-2) ----
+        double ah[3], bh[2];
 #pragma unroll
-            for (int n = 0; n < 6; ++n) p[n] = P[(6 + qr) * 12 + 6 + n];
+        for (int kk = 0; kk < 3; ++kk) ah[kk] = A_entry(4 * kk + lr, lc, ck, sk, dt);
+#pragma unroll
+        for (int kk = 1; kk < 3; ++kk) {
+            const int r = 4 * kk + lr;  // row of B^; rows 6-11 = Bt rows 0-5
+            const int m = (r >= 6 && r < 12) ? r - 6 : 0;
+            const double vb = Bt[m * 12 + (lc < 12 ? lc : 0)];
+            const double vd = sl[SO_DV + m];
+            bh[kk - 1] = (r >= 6 && r < 12) ? ((lc < 12) ? vb : (lc == 12) ? vd : 0.0) : 0.0;
+        }
+        // ---- C^ = P B^ ; PA = P A_k ----
+        d4 C = {0.0, 0.0, 0.0, 0.0}, PA = {0.0, 0.0, 0.0, 0.0};
+        C = MFMA64(P[1], bh[0], C);
+        C = MFMA64(P[2], bh[1], C);
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) PA = MFMA64(P[kk], ah[kk], PA);
+        // ---- Guu = Rr + B^' C^ (Rr: 3x3 leg blocks on the diagonal) ----
+        d4 G;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = lr + 4 * i;
+            const bool on = r < 12 && lc < 12 && (r / 3) == (lc / 3);
+            const int rr = r < 12 ? r : 0, cc = lc < 12 ? lc : 0;
+            const double v = sl[SO_RR + (rr / 3) * 9 + (rr % 3) * 3 + (cc % 3)];
+            G[i] = on ? v : 0.0;
+        }
+        G = MFMA64(bh[0], C[1], G);
+        G = MFMA64(bh[1], C[2], G);
+        // ---- out: v = C^[:, 12], Guu column-major for the elimination, Z = rows 6-11 of PA ----
+        if (lc < 12) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                double v = 0.0;
-#pragma unroll
-                for (int n = 0; n < 6; ++n) v += p[n] * Bt[n * 12 + 3 * qg + i];
-                S.C[qr * 12 + 3 * qg + i] = v;
+                const int r = lr + 4 * i;
+                S.GT[lc * 12 + r] = G[i];
+                if (r >= 6) g[GO_Z + (r - 6) * 12 + lc] = PA[i];
             }
-            if (qg < 2) {
+        } else if (lc == 12) {
 #pragma unroll
-                for (int i = 0; i < 3; ++i) g[GO_Z + qr * 12 + 3 * qg + i] = P[(6 + qr) * 12 + 3 * qg + i];
-            }
-        } else if (lane < 48) {
-            // PA6[r][3cg+i] = P[r][6+3cg+i] + dt sum_q P[r][3cg+q] W[q][i],  W = M(yaw) (cg 0) or I (cg 1)
-            double b[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) b[q] = P[rA * 12 + 3 * cgA + q];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                double m[3];
-                Mcol(ck, sk, i, m);
-                if (cgA) {
-                    m[0] = (i == 0) ? 1.0 : 0.0;
-                    m[1] = (i == 1) ? 1.0 : 0.0;
-                    m[2] = (i == 2) ? 1.0 : 0.0;
-                }
-                const double v = P[rA * 12 + 6 + 3 * cgA + i] + dt * (b[0] * m[0] + b[1] * m[1] + b[2] * m[2]);
-                S.PA6[rA * 6 + 3 * cgA + i] = v;
-                if (rA >= 6) g[GO_Z + (rA - 6) * 12 + 6 + 3 * cgA + i] = v;
-            }
-        } else if (lane < 60) {
-            const int r = lane - 48;
-            double v = 0.0;
-#pragma unroll
-            for (int n = 0; n < 6; ++n) v += P[r * 12 + 6 + n] * sl[SO_DV + n];
-            sl[SO_VV + r] = v;
+            for (int i = 0; i < 3; ++i) sl[SO_VV + lr + 4 * i] = C[i];
         }
         LMPC_SYNC();
         SUB(5);
-        // ---- level B: Guu (all 144 entries), column-major ----
-        if (lane < 48) {
-            double bt[6];
-#pragma unroll
-            for (int m = 0; m < 6; ++m) bt[m] = Bt[m * 12 + qr];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                double v = (qr3 == qg) ? sl[SO_RR + qg * 9 + qrm3 * 3 + i] : 0.0;
-#pragma unroll
-                for (int m = 0; m < 6; ++m) v += bt[m] * S.C[m * 12 + 3 * qg + i];
-                S.GT[(3 * qg + i) * 12 + qr] = v;
-            }
-        }
-        LMPC_SYNC();
-        SUB(6);
         // ---- block Cholesky elimination of [Guu | Bt' | I] -> [L' | V = L^-1 Bt' | L^-1] ----
         // lane j < 30 keeps column j in registers.  Per 3x3 leg block (one barrier each):
         // the pivot columns go to LDS; every lane factors the pivot block D = Ld Ld' itself,
@@ -368,14 +385,15 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 #pragma unroll
             for (int r = 0; r < 12; ++r) a[r] = fma(src[r], keep, (r == lane - 18) ? 1.0 : 0.0);
         }
+        // pivot columns of block 0
+        if (lane < 3) {
+#pragma unroll
+            for (int r = 0; r < 12; ++r) S.PNL[lane * 12 + r] = a[r];
+        }
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
             const int o = 3 * blk;
-            ldouble* pnl = S.PNL + (blk & 1) * 36;  // double-buffered: block b+1 writes while nobody reads block b's copy
-            if (lane >= o && lane < o + 3) {
-#pragma unroll
-                for (int r = o; r < 12; ++r) pnl[(lane - o) * 12 + r] = a[r];
-            }
+            const ldouble* pnl = S.PNL + (blk & 1) * 36;  // double-buffered: block b+1 publishes while b is read
             LMPC_SYNC();
             const double i00 = rsq_nr(pnl[o]);
             const double l10 = pnl[o + 1] * i00, l20 = pnl[o + 2] * i00;
@@ -389,119 +407,80 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
                 const double y2 = z2 * i22;
                 const double y1 = (z1 - l21 * y2) * i11;
                 const double y0 = (z0 - l10 * y1 - l20 * y2) * i00;
+                // next block's rows first, so its pivot columns can be published before the rest
 #pragma unroll
-                for (int r = o + 3; r < 12; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
+                for (int r = o + 3; r < o + 6; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
+                if (lane >= o + 3 && lane < o + 6) {
+                    ldouble* nx = S.PNL + ((blk + 1) & 1) * 36 + (lane - o - 3) * 12;
+#pragma unroll
+                    for (int r = o + 3; r < o + 6; ++r) nx[r] = a[r];
+                }
+#pragma unroll
+                for (int r = o + 6; r < 12; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
+                if (lane >= o + 3 && lane < o + 6) {
+                    ldouble* nx = S.PNL + ((blk + 1) & 1) * 36 + (lane - o - 3) * 12;
+#pragma unroll
+                    for (int r = o + 6; r < 12; ++r) nx[r] = a[r];
+                }
             }
             a[o] = z0;
             a[o + 1] = z1;
             a[o + 2] = z2;
+            SUB(9 + blk);
         }
-        // V (lanes 12-17) and L^-1 (lanes 18-29) out
-        if (lane >= 12 && lane < 18) {
+        // out, branch-free: lanes 12-17 -> V (LDS + global), lanes 18-29 -> packed L^-1 (upper-triangle
+        // entries and idle lanes go to the stage's dummy slot)
+        {
+            const bool isv = lane >= 12 && lane < 18, isl = lane >= 18 && lane < 30;
+            const int m = isv ? lane - 12 : 0, c = isl ? lane - 18 : 0;
+            ldouble* vl = isv ? S.VL + m * 12 : S.pa;
 #pragma unroll
             for (int r = 0; r < 12; ++r) {
-                S.VL[(lane - 12) * 12 + r] = a[r];
-                g[GO_V + (lane - 12) * 12 + r] = a[r];
+                const int gi = isv ? GO_V + m * 12 + r : (isl && r >= c) ? GO_LINV + r * (r + 1) / 2 + c : GO_DUMMY;
+                g[gi] = a[r];
+                vl[isv ? r : 0] = a[r];
             }
-        } else if (lane >= 18 && lane < 30) {
-            const int c = lane - 18;
-#pragma unroll
-            for (int r = 0; r < 12; ++r)
-                if (r >= c) g[GO_LINV + r * (r + 1) / 2 + c] = a[r];
         }
         LMPC_SYNC();
         SUB(7);
-        // ---- level D: K = V'V ----
-        if (lane < 36) {
-            double v = 0.0;
+        // ---- K^ = V^' V^ (V^ = [0 | V], columns 6-11) ----
+        d4 KH = {0.0, 0.0, 0.0, 0.0};
+        {
+            const bool vc = lc >= 6 && lc < 12;
+            const int m = vc ? lc - 6 : 0;
 #pragma unroll
-            for (int r = 0; r < 12; ++r) v += S.VL[dm * 12 + r] * S.VL[dn * 12 + r];
-            S.K[lane] = v;
-            g[GO_K + lane] = v;
-        }
-        LMPC_SYNC();
-        SUB(8);
-        // ---- level E: KZ = K Z ; closed-loop N_k = A_k - [0; KZ] into the stage slot ----
-        if (lane < 24) {
-            const bool lo = qg < 2;
-            const ldouble* zb = lo ? P + 72 + 3 * qg : S.PA6 + 36 + 3 * (qg - 2);
-            const int zs = lo ? 12 : 6;
-            double kk[6];
-#pragma unroll
-            for (int n = 0; n < 6; ++n) kk[n] = S.K[qr * 6 + n];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                double v = 0.0;
-#pragma unroll
-                for (int n = 0; n < 6; ++n) v += kk[n] * zb[n * zs + i];
-                S.KZ[qr * 12 + 3 * qg + i] = v;
-                sl[SO_N + (6 + qr) * 12 + 3 * qg + i] = ((6 + qr == 3 * qg + i) ? 1.0 : 0.0) - v;
-            }
-        } else if (lane < 48) {
-            // rows 0-5 of A_k: [I  0  dt M(yaw)  0 ; 0  I  0  dt I]
-            const int ra = (lane - 24) >> 2, cg = (lane - 24) & 3;
-            double mrow[3];  // row ra of M (rows 0-2 only)
-            mrow[0] = (ra == 0) ? ck : (ra == 1) ? -sk : 0.0;
-            mrow[1] = (ra == 0) ? sk : (ra == 1) ? ck : 0.0;
-            mrow[2] = (ra == 2) ? 1.0 : 0.0;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int c = 3 * cg + i;
-                double v = (ra == c) ? 1.0 : 0.0;
-                if (ra < 3 && cg == 2) v += dt * mrow[i];
-                if (ra >= 3 && cg == 3 && c == ra + 6) v += dt;
-                sl[SO_N + ra * 12 + c] = v;
+            for (int kk = 0; kk < 3; ++kk) {
+                const double v = S.VL[m * 12 + 4 * kk + lr];
+                const double vh = vc ? v : 0.0;
+                KH = MFMA64(vh, vh, KH);
             }
         }
-        LMPC_SYNC();
-        SUB(9);
-        // ---- level F: P_k = Q + A'PA - Z'(KZ) ----
+        // ---- KZ^ = K^ PA (k-blocks 1-2: K^ is zero outside rows/columns 6-11) ----
+        d4 KZ = {0.0, 0.0, 0.0, 0.0};
+        KZ = MFMA64(KH[1], PA[1], KZ);
+        KZ = MFMA64(KH[2], PA[2], KZ);
+        // K -> global (for the vector pass), N_k = A_k - KZ^ -> stage slot
+        if (lc >= 6 && lc < 12) {
+#pragma unroll
+            for (int i = 1; i < 3; ++i) {
+                const int r = lr + 4 * i;
+                if (r >= 6) g[GO_K + (r - 6) * 6 + (lc - 6)] = KH[i];
+            }
+        }
+        if (lc < 12) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) sl[SO_N + (lr + 4 * i) * 12 + lc] = ah[i] - KZ[i];
+        }
+        // ---- P_k = Q + A'PA - PA' KZ^ ----
         if (k > 0) {
-            if (lane < 48) {
-                const bool rlo = qr < 6, clo = qg < 2;
-                // Z[m][qr]
-                const ldouble* zr = rlo ? P + 72 + qr : S.PA6 + 36 + (qr - 6);
-                const int zs = rlo ? 12 : 6;
-                double zc[6];
+            d4 Pn = Qd;
 #pragma unroll
-                for (int m = 0; m < 6; ++m) zc[m] = zr[m * zs];
-                // A'PA[qr][3qg+i]
-                const ldouble* ab;
-                int as;
-                if (clo) {
-                    ab = rlo ? P + qr * 12 + 3 * qg : S.PA6 + 3 * qg * 6 + (qr - 6);
-                    as = rlo ? 1 : 6;
-                } else {
-                    ab = S.PA6 + qr * 6 + 3 * (qg - 2);
-                    as = 1;
-                }
-                // bottom-right block: + dt sum_q Wr[q] PA6[3rg+q][c-6]
-                const bool br = !rlo && !clo;
-                const int rp = rlo ? 0 : qr - 6, rg = rp / 3;
-                double wr[3];
-                Mcol(ck, sk, rp, wr);  // M[q][rp] for rp < 3
-                if (rg) {
-                    wr[0] = (rp == 3) ? 1.0 : 0.0;
-                    wr[1] = (rp == 4) ? 1.0 : 0.0;
-                    wr[2] = (rp == 5) ? 1.0 : 0.0;
-                }
-                const ldouble* cb = S.PA6 + (br ? 3 * rg * 6 + 3 * (qg - 2) : 0);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    double v = ab[i * as] + qdiag[i];
-                    const double corr = cb[i] * wr[0] + cb[6 + i] * wr[1] + cb[12 + i] * wr[2];
-                    v += br ? dt * corr : 0.0;
-#pragma unroll
-                    for (int m = 0; m < 6; ++m) v -= zc[m] * S.KZ[m * 12 + 3 * qg + i];
-                    Pn[qr * 12 + 3 * qg + i] = v;
-                }
-            }
-            LMPC_SYNC();
-            SUB(10);
-            ldouble* t = P;
+            for (int kk = 0; kk < 3; ++kk) Pn = MFMA64(ah[kk], PA[kk], Pn);
+            Pn = MFMA64(-PA[1], KZ[1], Pn);
+            Pn = MFMA64(-PA[2], KZ[2], Pn);
             P = Pn;
-            Pn = t;
         }
+        SUB(8);
     }
 }
 

@@ -34,7 +34,8 @@ rnd = (it[:n] >> 16).astype(float)
 nfac = ipm + rnd  # one factorisation per IPM iteration (+ the final check) and per polish round (approx.)
 nsol = 2 * ipm + rnd
 sub = {0: "solve:pre", 1: "solve:backward", 2: "solve:mid", 3: "solve:forward", 4: "solve:post",
-       5: "factor:A", 6: "factor:B", 7: "factor:elim+out", 8: "factor:D(K)", 9: "factor:E(KZ)", 10: "factor:F(P)"}
+       5: "factor:pre-MFMA", 9: "factor:elim blk0", 10: "factor:elim blk1", 11: "factor:elim blk2", 12: "factor:elim blk3",
+       7: "factor:elim out", 8: "factor:post-MFMA"}
 print(f"sub-phases (cycles per QP, per call; H={H})")
 for i, nm in sub.items():
     per_qp = sb[:, i].mean()
