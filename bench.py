@@ -174,6 +174,9 @@ def main():
             "qp_status": {"converged": int(stats[0]), "max_iter": int(stats[1]), "nan": int(stats[2])},
             "ipm_iters_mean": ipm_mean,
             "polish_rounds_mean": pol_mean,
+            "ipm_iters_max": int(np.max(it & 0xFFFF)),
+            "polish_rounds_max": int(np.max(it >> 16)),
+            "ipm_iters_p99": float(np.percentile(it & 0xFFFF, 99)),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -60,6 +60,19 @@ def build_stamps(force: bool = False) -> str:
     return out
 
 
+def build_variant(tag: str, defines, force: bool = False) -> str:
+    """Diagnostic library variant (extra -D flags) under tools/build/; never shipped as the product."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    out = os.path.join(ROOT, "tools", "build", f"liblmpc_{tag}.so")
+    if not force and not _stale(out, srcs + [os.path.join(CSRC, h) for h in HEADERS]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wno-unused-result",
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + [f"-D{d}" for d in defines] + srcs
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_cpp_test(force: bool = False) -> str:
     """C++ program that drives legged::ConvexQPSolver exactly like ConvexMpc::grf_update."""
     src = os.path.join(ROOT, "tests", "cpp", "grf_update_test.cpp")

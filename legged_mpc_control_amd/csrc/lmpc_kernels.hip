@@ -996,13 +996,20 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         st[t] = valid[t] && contact[(size_t)qp * 4 * H + ls] != 0;
         nst_loc += st[t] ? 1 : 0;
         f[t][0] = f[t][1] = 0.0;
-        f[t][2] = st[t] ? 0.5 * fzmax : 0.0;
+        {
+            // starting point: each stance leg carries its share of the weight (fz = m g / n_stance,
+            // capped at fmax/2), zero tangential force; slacks from the constraints and a
+            // centred z = 1/s (s z = 1).  Measured: ~0.9 fewer interior-point iterations on
+            // average than fz = fmax/2, z = 1 (tools/variant_sweep.py, profiles/r01_init_sweep.log).
+            const double cnt = quad_sum(st[t] ? 1.0 : 0.0);  // stance legs of this stage (all lanes: DPP)
+            f[t][2] = st[t] ? fmin(0.5 * fzmax, prm.mass * prm.grav / fmax(cnt, 1.0)) : 0.0;
+        }
         double o[5];
         cons_resid(f[t], mu, fzmax, o);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
             s[t][i] = st[t] ? -o[i] : 1.0;
-            z[t][i] = 1.0;
+            z[t][i] = 1.0 / s[t][i];
         }
         u[t][0] = u[t][1] = u[t][2] = 0.0;
     }
