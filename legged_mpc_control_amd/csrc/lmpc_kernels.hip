@@ -289,19 +289,19 @@ __device__ __forceinline__ double Atw_el(Ptr w, int r, double ck, double sk, dou
 // every product feeds the next without an LDS round trip:
 //   C^ = P B^            (B^ = [0; Bt | dv]: rows 6-11 hold Bt, column 12 dv -> v = P d)
 //   Guu = Rr + B^' C^     (the 12x12 input Hessian block plus the lifted state cost)
-//   PA = P A_k
+//   PA = P A_k = P + P (dt N)         (dt N: rows 0-5 only -> 2 k-blocks)
 //   [block Cholesky of Guu with [Bt' | I] eliminated alongside, VALU, one column per lane]
 //   K^ = V^' V^           (V^ = [0 | V]: K lands in rows/columns 6-11, aligned with PA's rows)
 //   KZ^ = K^ PA           (rows 6-11 = K Z,  Z = P2 A = rows 6-11 of PA)
-//   P_k = Q + A'PA - PA' KZ^ ;  N_k = A_k - KZ^ (closed-loop matrix for the vector pass)
+//   P_k = Q + PA + (dt N)'PA - PA' KZ^ ;  N_k = A_k - KZ^ (closed-loop matrix for the vector pass)
 // ---------------------------------------------------------------------------
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
-// entry (r, c) of A_k = I + dt N(yaw) (zero padding outside 12x12)
-__device__ __forceinline__ double A_entry(int r, int c, double ck, double sk, double dt) {
+// entry (r, c) of dt N(yaw) = A_k - I (nonzero only in rows 0-5, columns 6-11)
+__device__ __forceinline__ double dtN_entry(int r, int c, double ck, double sk, double dt) {
     if (r >= 12 || c >= 12) return 0.0;
-    double v = (r == c) ? 1.0 : 0.0;
+    double v = 0.0;
     if (r < 3 && c >= 6 && c < 9) {
         const int j = c - 6;
         const double m = (r == 0) ? ((j == 0) ? ck : (j == 1) ? sk : 0.0)
@@ -329,10 +329,10 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         ldouble* sl = S.st + k * SK;
         gdouble* g = gs + k * GS;
         const ldouble* Bt = sl + SO_BT;
-        // ---- operands: A_k (k-blocks 0-2) and B^ (k-blocks 1-2) ----
-        double ah[3], bh[2];
+        // ---- operands: dt N(yaw) (k-blocks 0-1: rows 0-7) and B^ (k-blocks 1-2) ----
+        double nh[2], bh[2];
 #pragma unroll
-        for (int kk = 0; kk < 3; ++kk) ah[kk] = A_entry(4 * kk + lr, lc, ck, sk, dt);
+        for (int kk = 0; kk < 2; ++kk) nh[kk] = dtN_entry(4 * kk + lr, lc, ck, sk, dt);
 #pragma unroll
         for (int kk = 1; kk < 3; ++kk) {
             const int r = 4 * kk + lr;  // row of B^; rows 6-11 = Bt rows 0-5
@@ -341,12 +341,13 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
             const double vd = sl[SO_DV + m];
             bh[kk - 1] = (r >= 6 && r < 12) ? ((lc < 12) ? vb : (lc == 12) ? vd : 0.0) : 0.0;
         }
-        // ---- C^ = P B^ ; PA = P A_k ----
-        d4 C = {0.0, 0.0, 0.0, 0.0}, PA = {0.0, 0.0, 0.0, 0.0};
+        // ---- C^ = P B^ ; PA = P A_k = P + P (dt N) ----
+        d4 C = {0.0, 0.0, 0.0, 0.0};
         C = MFMA64(P[1], bh[0], C);
         C = MFMA64(P[2], bh[1], C);
-#pragma unroll
-        for (int kk = 0; kk < 3; ++kk) PA = MFMA64(P[kk], ah[kk], PA);
+        d4 PA = P;
+        PA = MFMA64(P[0], nh[0], PA);
+        PA = MFMA64(P[1], nh[1], PA);
         // ---- Guu = Rr + B^' C^ (Rr: 3x3 leg blocks on the diagonal) ----
         d4 G;
 #pragma unroll
@@ -469,13 +470,17 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         }
         if (lc < 12) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) sl[SO_N + (lr + 4 * i) * 12 + lc] = ah[i] - KZ[i];
+            for (int i = 0; i < 3; ++i) {
+                const int r = lr + 4 * i;
+                const double av = ((r == lc) ? 1.0 : 0.0) + (i < 2 ? nh[i < 2 ? i : 0] : 0.0);  // A_k = I + dt N
+                sl[SO_N + r * 12 + lc] = av - KZ[i];
+            }
         }
-        // ---- P_k = Q + A'PA - PA' KZ^ ----
+        // ---- P_k = Q + A'PA - PA' KZ^,  A'PA = PA + (dt N)' PA ----
         if (k > 0) {
-            d4 Pn = Qd;
-#pragma unroll
-            for (int kk = 0; kk < 3; ++kk) Pn = MFMA64(ah[kk], PA[kk], Pn);
+            d4 Pn = Qd + PA;
+            Pn = MFMA64(nh[0], PA[0], Pn);
+            Pn = MFMA64(nh[1], PA[1], Pn);
             Pn = MFMA64(-PA[1], KZ[1], Pn);
             Pn = MFMA64(-PA[2], KZ[2], Pn);
             P = Pn;

@@ -7,10 +7,10 @@ import sys
 
 
 def classify(op):
-    if op.startswith("v_") and ("f64" in op or "_b64" in op and op.startswith("v_mov_b64")):
-        return "v64"
     if op.startswith("v_mfma"):
         return "mfma"
+    if op.startswith("v_") and ("f64" in op or "_b64" in op and op.startswith("v_mov_b64")):
+        return "v64"
     if op.startswith("v_"):
         return "v32"
     if op.startswith("ds_"):
