@@ -174,7 +174,8 @@ constexpr int SO_N6 = 312;   // 6   K s2 + psi - dv (later: q2)
 constexpr int SO_PN = 318;   // 12  p_{k+1}
 constexpr int SO_XS = 330;   // 12  x_k
 constexpr int SO_LAM = 342;  // 12  lambda_{k+1}
-constexpr int SK = 354;
+constexpr int SO_ACT = 354;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
+constexpr int SK = 358;
 // global scratch per stage
 constexpr int GO_LINV = 0;   // 78 packed L^-1 (lower, row-packed)
 constexpr int GO_V = 78;     // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
@@ -386,15 +387,28 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 #pragma unroll
             for (int r = 0; r < 12; ++r) a[r] = fma(src[r], keep, (r == lane - 18) ? 1.0 : 0.0);
         }
-        // pivot columns of block 0
-        if (lane < 3) {
-#pragma unroll
-            for (int r = 0; r < 12; ++r) S.PNL[lane * 12 + r] = a[r];
+        // Leg blocks with T = 0 (swing legs; apex legs in the polish) have Guu block = I and no
+        // coupling (their Bt columns and off-diagonal Rr are exactly zero): their elimination step
+        // is the identity and is skipped.  amask is wave-uniform (scalar branches).
+        int amask;
+        {
+            const double f0 = sl[SO_ACT], f1 = sl[SO_ACT + 1], f2 = sl[SO_ACT + 2], f3 = sl[SO_ACT + 3];
+            amask = (f0 != 0.0 ? 1 : 0) | (f1 != 0.0 ? 2 : 0) | (f2 != 0.0 ? 4 : 0) | (f3 != 0.0 ? 8 : 0);
+            amask = __builtin_amdgcn_readfirstlane(amask);
         }
+        if (amask) {  // pivot columns of the first coupled block
+            const int b0 = __builtin_ctz(amask);
+            if (lane >= 3 * b0 && lane < 3 * b0 + 3) {
+#pragma unroll
+                for (int r = 0; r < 12; ++r) S.PNL[(lane - 3 * b0) * 12 + r] = a[r];
+            }
+        }
+        int par = 0;  // PNL buffer in use (double-buffered: the next block publishes while this one is read)
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
+            if (!((amask >> blk) & 1)) continue;
             const int o = 3 * blk;
-            const ldouble* pnl = S.PNL + (blk & 1) * 36;  // double-buffered: block b+1 publishes while b is read
+            const ldouble* pnl = S.PNL + par * 36;
             LMPC_SYNC();
             const double i00 = rsq_nr(pnl[o]);
             const double l10 = pnl[o + 1] * i00, l20 = pnl[o + 2] * i00;
@@ -404,22 +418,24 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
             const double z0 = i00 * a[o];
             const double z1 = (a[o + 1] - l10 * z0) * i11;
             const double z2 = (a[o + 2] - l20 * z0 - l21 * z1) * i22;
-            if (blk < 3) {
+            const int rest = amask >> (blk + 1);  // coupled blocks still to come
+            if (blk < 3 && rest) {
                 const double y2 = z2 * i22;
                 const double y1 = (z1 - l21 * y2) * i11;
                 const double y0 = (z0 - l10 * y1 - l20 * y2) * i00;
-                // next block's rows first, so its pivot columns can be published before the rest
+                const int nb = blk + 1 + __builtin_ctz(rest);
+                // the next coupled block's rows first, then publish its pivot columns, then the rest
 #pragma unroll
                 for (int r = o + 3; r < o + 6; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
-                if (lane >= o + 3 && lane < o + 6) {
-                    ldouble* nx = S.PNL + ((blk + 1) & 1) * 36 + (lane - o - 3) * 12;
+                const bool pub = lane >= 3 * nb && lane < 3 * nb + 3;
+                ldouble* nx = S.PNL + (par ^ 1) * 36 + (pub ? (lane - 3 * nb) * 12 : 0);
+                if (pub && nb == blk + 1) {
 #pragma unroll
                     for (int r = o + 3; r < o + 6; ++r) nx[r] = a[r];
                 }
 #pragma unroll
                 for (int r = o + 6; r < 12; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
-                if (lane >= o + 3 && lane < o + 6) {
-                    ldouble* nx = S.PNL + ((blk + 1) & 1) * 36 + (lane - o - 3) * 12;
+                if (pub) {
 #pragma unroll
                     for (int r = o + 6; r < 12; ++r) nx[r] = a[r];
                 }
@@ -427,6 +443,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
             a[o] = z0;
             a[o + 1] = z1;
             a[o + 2] = z2;
+            par ^= 1;
             SUB(9 + blk);
         }
         // out, branch-free: lanes 12-17 -> V (LDS + global), lanes 18-29 -> packed L^-1 (upper-triangle
@@ -811,6 +828,7 @@ __device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const S
         const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
 #pragma unroll
         for (int e = 0; e < 9; ++e) sl[SO_RR + j * 9 + e] = on * R3[e] + ((e % 4 == 0) ? off : 0.0);
+        sl[SO_ACT + j] = on;
 #pragma unroll
         for (int m = 0; m < 6; ++m)
 #pragma unroll
@@ -838,6 +856,7 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
             bool fixed[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) fixed[a] = (T[t][a] == 0.0 && T[t][3 + a] == 0.0 && T[t][6 + a] == 0.0);
+            sl[SO_ACT + j] = (fixed[0] && fixed[1] && fixed[2]) ? 0.0 : 1.0;
             double RT[9];  // Rt T
 #pragma unroll
             for (int p = 0; p < 3; ++p)
