@@ -62,8 +62,8 @@ __device__ unsigned long long lmpc_stamps[STAMP_QPS][8];
 #define STAMP_DECL unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long _st_t0 = __builtin_readcyclecounter();
 #define STAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _st_acc[i] += _t - _st_t0; _st_t0 = _t; } while (0)
 #define STAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < STAMP_QPS) for (int _i = 0; _i < 8; ++_i) lmpc_stamps[qp][_i] = _st_acc[_i]; } while (0)
-// sub-phase stamps inside the outlined factor / solve functions (slot < 16)
-__device__ unsigned long long lmpc_substamps[STAMP_QPS][16];
+// sub-phase stamps inside the outlined factor / solve functions and the main loop (slot < 24)
+__device__ unsigned long long lmpc_substamps[STAMP_QPS][24];
 #define SUB_DECL unsigned long long _sb_t0 = __builtin_readcyclecounter();
 #define SUB(i) do { const unsigned long long _t = __builtin_readcyclecounter(); \
     if (threadIdx.x == 0 && blockIdx.x < STAMP_QPS) \
@@ -915,6 +915,31 @@ __device__ __forceinline__ void leg_rhs(const Smem& S, const bool (&valid)[LS], 
     }
 }
 
+// interior-point variants (T = I for a stance leg, 0 for a swing leg; up = 0): rr = rt, u = y
+template <int LS>
+__device__ __forceinline__ void leg_rhs_ipm(const Smem& S, const bool (&valid)[LS], const bool (&st)[LS],
+                                            const int (&lsk)[LS], const int (&lsj)[LS], const double (&rt)[LS][3]) {
+#pragma unroll
+    for (int t = 0; t < LS; ++t) {
+        if (!valid[t]) continue;
+        ldouble* rr = S.st + lsk[t] * SK + SO_RRV + 3 * lsj[t];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) rr[a] = st[t] ? rt[t][a] : 0.0;
+    }
+}
+template <int LS>
+__device__ __forceinline__ void leg_u_ipm(const Smem& S, const bool (&valid)[LS], const bool (&st)[LS],
+                                          const int (&lsk)[LS], const int (&lsj)[LS], double (&u)[LS][3]) {
+#pragma unroll
+    for (int t = 0; t < LS; ++t) {
+        u[t][0] = u[t][1] = u[t][2] = 0.0;
+        if (!valid[t] || !st[t]) continue;
+        const ldouble* y = S.st + lsk[t] * SK + SO_RRV + 3 * lsj[t];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) u[t][p] = y[p];
+    }
+}
+
 // u = up + T y (y from SO_RRV after riccati_solve)
 template <int LS>
 __device__ __forceinline__ void leg_u(const Smem& S, const bool (&valid)[LS], const int (&lsk)[LS], const int (&lsj)[LS],
@@ -1052,12 +1077,11 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         int mode = PRED;
         int act[LS];
         bool apex[LS];
-        double dsa[LS][5], dza[LS][5], is[LS][5];
+        double ua[LS][3];  // predictor step u_aff: the only predictor state kept across the corrector solve
 #pragma unroll
-        for (int t = 0; t < LS; ++t)
-#pragma unroll
-            for (int i = 0; i < 5; ++i) is[t][i] = 0.0;
+        for (int t = 0; t < LS; ++t) ua[t][0] = ua[t][1] = ua[t][2] = 0.0;
         double mu_c = 0.0, smu = 0.0;
+        SUB_DECL
         for (;;) {
             if (mode == PRED) {
                 double loc = 0.0;
@@ -1089,8 +1113,8 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                         if (st[t]) {
 #pragma unroll
                             for (int i = 0; i < 5; ++i) {
-                                is[t][i] = rcp_nr(s[t][i]);  // 1/s, reused by the whole predictor-corrector step
-                                W[i] = z[t][i] * is[t][i];
+                                W[i] = z[t][i] * rcp_nr(s[t][i]);  // 1/s is recomputed where needed: keeping it
+                                                                    // live across the factor/solve calls spills it
                                 wv[i] = W[i] * (s[t][i] - (i == 4 ? fzmax : 0.0));
                             }
                         }
@@ -1103,9 +1127,6 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                         Rt[t][4] = mu * (W[2] - W[3]);
                         Rt[t][5] = prm.r[3 * j + 2] + mu * mu * (sx + sy) + W[4];
                         cons_tw(wv, mu, rt[t]);
-#pragma unroll
-                        for (int i = 0; i < 9; ++i) T[t][i] = (st[t] && (i % 4 == 0)) ? 1.0 : 0.0;
-                        up[t][0] = up[t][1] = up[t][2] = 0.0;
                     }
                 }
             }
@@ -1130,10 +1151,13 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                     rt[t][0] = rt[t][1] = rt[t][2] = 0.0;
                 }
             }
+            SUB(13);  // (diagnostic) leg-step bookkeeping since the previous solve
             if (mode == PRED) leg_stage_prep_ipm<LS>(prm, S, valid, st, lsk, lsj, Rt);
             else if (mode == POLISH) leg_stage_prep<LS>(prm, S, valid, lsk, lsj, Rt, T, up);
-            leg_rhs<LS>(S, valid, lsk, lsj, Rt, rt, T, up);
+            if (mode == POLISH) leg_rhs<LS>(S, valid, lsk, lsj, Rt, rt, T, up);
+            else leg_rhs_ipm<LS>(S, valid, st, lsk, lsj, rt);
             LMPC_SYNC();
+            SUB(14);  // (diagnostic) stage prep + rhs
             STAMP(1);  // leg-step work (IPM/polish bookkeeping, stage prep)
             if (mode != CORR) riccati_factor(S, (gdouble*)gs, H, dt, lane);
             STAMP(2);  // factorisation
@@ -1146,20 +1170,26 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                 default: riccati_solve<6>(S, (const gdouble*)gs, H, dt, lane); break;
             }
             STAMP(3);  // vector pass
-            leg_u<LS>(S, valid, lsk, lsj, T, up, u);
+            SUB(15);   // (diagnostic) factor + solve, already split by their own stamps
+            if (mode == POLISH) leg_u<LS>(S, valid, lsk, lsj, T, up, u);
+            else leg_u_ipm<LS>(S, valid, st, lsk, lsj, u);
+            SUB(16);   // (diagnostic) leg_u
             if (mode == PRED) {
                 double amax = 1.0;
+                double dsa[LS][5], dza[LS][5];
 #pragma unroll
                 for (int t = 0; t < LS; ++t) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) dsa[t][i] = dza[t][i] = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) ua[t][m] = u[t][m];
                     if (!st[t]) continue;
                     double o[5];
                     cons_resid(u[t], mu, fzmax, o);
 #pragma unroll
                     for (int i = 0; i < 5; ++i) {
                         dsa[t][i] = -o[i] - s[t][i];
-                        dza[t][i] = -z[t][i] - z[t][i] * is[t][i] * dsa[t][i];
+                        dza[t][i] = -z[t][i] - z[t][i] * rcp_nr(s[t][i]) * dsa[t][i];
                         // fraction to the boundary: the hardware reciprocal estimate is ample here
                         if (dsa[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(dsa[t][i]));
                         if (dza[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dza[t][i]));
@@ -1181,10 +1211,11 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                     double wv[5];
 #pragma unroll
                     for (int i = 0; i < 5; ++i)
-                        wv[i] = (z[t][i] * (s[t][i] - (i == 4 ? fzmax : 0.0)) + smu - dsa[t][i] * dza[t][i]) * is[t][i];
+                        wv[i] = (z[t][i] * (s[t][i] - (i == 4 ? fzmax : 0.0)) + smu - dsa[t][i] * dza[t][i]) * rcp_nr(s[t][i]);
                     cons_tw(wv, mu, rt[t]);
                 }
                 mode = CORR;
+                SUB(17);  // (diagnostic) predictor post-step
             } else if (mode == CORR) {
                 double ds[LS][5], dz[LS][5];
                 double amax = 1.0;
@@ -1193,12 +1224,16 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
 #pragma unroll
                     for (int i = 0; i < 5; ++i) ds[t][i] = dz[t][i] = 0.0;
                     if (!st[t]) continue;
-                    double o[5];
+                    double o[5], oa[5];
                     cons_resid(u[t], mu, fzmax, o);
+                    cons_resid(ua[t], mu, fzmax, oa);
 #pragma unroll
                     for (int i = 0; i < 5; ++i) {
+                        const double is = rcp_nr(s[t][i]);
+                        const double dsa = -oa[i] - s[t][i];  // predictor step, recomputed from u_aff
+                        const double dza = -z[t][i] - z[t][i] * is * dsa;
                         ds[t][i] = -o[i] - s[t][i];
-                        dz[t][i] = (smu - z[t][i] * s[t][i] - dsa[t][i] * dza[t][i] - z[t][i] * ds[t][i]) * is[t][i];
+                        dz[t][i] = (smu - z[t][i] * s[t][i] - dsa * dza - z[t][i] * ds[t][i]) * is;
                         if (ds[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(ds[t][i]));
                         if (dz[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dz[t][i]));
                     }
@@ -1217,6 +1252,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                 }
                 ++ipm_it;
                 mode = PRED;
+                SUB(18);  // (diagnostic) corrector post-step
             } else {
                 // ---- polish verification: primal feasibility + multiplier signs ----
                 STAMP(1);
@@ -1378,7 +1414,7 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
 #ifdef LMPC_STAMPS
 extern "C" int lmpc_debug_substamps(unsigned long long* out, int nqp) {
     if (nqp > STAMP_QPS) nqp = STAMP_QPS;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_substamps), (size_t)nqp * 16 * sizeof(unsigned long long)) == hipSuccess ? nqp : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_substamps), (size_t)nqp * 24 * sizeof(unsigned long long)) == hipSuccess ? nqp : -1;
 }
 extern "C" int lmpc_debug_stamps(unsigned long long* out, int nqp) {
     if (nqp > STAMP_QPS) nqp = STAMP_QPS;

@@ -26,7 +26,7 @@ for i, nm in enumerate(names):
 
 # sub-phase stamps (accumulated over every launch above: 2 runs)
 L.lmpc_debug_substamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-sb = np.zeros((min(count, 4096), 16), dtype=np.uint64)
+sb = np.zeros((min(count, 4096), 24), dtype=np.uint64)
 n = L.lmpc_debug_substamps(sb.ctypes.data, sb.shape[0])
 sb = sb[:n].astype(float) / 2.0
 ipm = (it[:n] & 0xffff).astype(float)
@@ -35,9 +35,11 @@ nfac = ipm + rnd  # one factorisation per IPM iteration (+ the final check) and 
 nsol = 2 * ipm + rnd
 sub = {0: "solve:pre", 1: "solve:backward", 2: "solve:mid", 3: "solve:forward", 4: "solve:post",
        5: "factor:pre-MFMA", 9: "factor:elim blk0", 10: "factor:elim blk1", 11: "factor:elim blk2", 12: "factor:elim blk3",
-       7: "factor:elim out", 8: "factor:post-MFMA"}
+       7: "factor:elim out", 8: "factor:post-MFMA", 13: "leg:top-of-loop", 14: "leg:prep+rhs",
+       16: "leg:leg_u", 17: "leg:pred-post", 18: "leg:corr-post"}
 print(f"sub-phases (cycles per QP, per call; H={H})")
 for i, nm in sub.items():
     per_qp = sb[:, i].mean()
-    calls = (nsol if i < 5 else nfac).mean()
+    calls = (nsol if (i < 5 or i >= 13) else nfac).mean()
+    calls = ipm.mean() if i in (17, 18) else calls
     print(f"  {nm:16s} {per_qp:12.0f}  per call {per_qp / calls:9.0f}  per stage {per_qp / calls / H:8.0f}")
