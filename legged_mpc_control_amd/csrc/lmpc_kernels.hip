@@ -603,33 +603,32 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
     }
     LMPC_SYNC();
     SUB(0);
-    // ---- backward: p_k = N_k' p_{k+1} + cst'_k (into stage k-1's PN slot); column r of N_k is
-    // fetched one step ahead so only the broadcast reads of p_{k+1} sit on the critical path ----
+    // ---- backward: p_k = N_k' p_{k+1} + cst'_k (into stage k-1's PN slot).  Row r is split over the
+    // 4 lanes (r, part): each sums 3 of the 12 terms, a DPP quad reduction combines them.  The lane's
+    // 3 entries of N_k are fetched one step ahead, so only 3 broadcast reads of p_{k+1} sit on the
+    // critical path ----
     {
-        const int r = lane < 12 ? lane : 0;
-        const bool act = lane < 12;
-        double nc[12];
+        const int r = (lane < 48) ? (lane >> 2) : 0, part = lane & 3, j0 = 3 * part;
+        const bool wr = lane < 48 && part == 0;
+        double nc[3];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) nc[j] = S.st[(H - 1) * SK + SO_N + j * 12 + r];
+        for (int q = 0; q < 3; ++q) nc[q] = S.st[(H - 1) * SK + SO_N + (j0 + q) * 12 + r];
         for (int k = H - 1; k >= 1; --k) {
             const ldouble* sl = S.st + k * SK;
-            // the reads this step waits for are issued first (LDS returns in order), the prefetch after
-            double pv[12];
+            double pv[3];
 #pragma unroll
-            for (int j = 0; j < 12; ++j) pv[j] = sl[SO_PN + j];
+            for (int q = 0; q < 3; ++q) pv[q] = sl[SO_PN + j0 + q];
             const double cst = sl[SO_CST + r];
-            double nn[12];
+            double nn[3];
             const ldouble* nxt = S.st + (k > 1 ? k - 1 : 1) * SK + SO_N + r;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) nn[j] = nxt[j * 12];
-            const double a0 = cst + nc[0] * pv[0] + nc[1] * pv[1] + nc[2] * pv[2] + nc[3] * pv[3];
-            const double a1 = nc[4] * pv[4] + nc[5] * pv[5] + nc[6] * pv[6] + nc[7] * pv[7];
-            const double a2 = nc[8] * pv[8] + nc[9] * pv[9] + nc[10] * pv[10] + nc[11] * pv[11];
-            // branch-free: idle lanes write a dummy word (a branch would sink the reads behind the prefetch)
-            ldouble* dst = act ? S.st + (k - 1) * SK + SO_PN + r : S.pa;
-            *dst = a0 + (a1 + a2);
+            for (int q = 0; q < 3; ++q) nn[q] = nxt[(j0 + q) * 12];
+            double v = nc[0] * pv[0] + nc[1] * pv[1] + nc[2] * pv[2];
+            v = quad_sum(v);
+            ldouble* dst = wr ? S.st + (k - 1) * SK + SO_PN + r : S.pa;  // branch-free: others write a dummy word
+            *dst = v + cst;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) nc[j] = nn[j];
+            for (int q = 0; q < 3; ++q) nc[q] = nn[q];
             LMPC_SYNC();
         }
     }
@@ -646,33 +645,32 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
     if (lane < 12) S.st[SO_XS + lane] = S.hdr[lane];
     LMPC_SYNC();
     SUB(2);
-    // ---- forward: x_{k+1} = N_k x_k - [0; n6'_k]; row r of N_{k+1} is fetched one step ahead ----
+    // ---- forward: x_{k+1} = N_k x_k - [0; n6'_k]; row r split over 4 lanes as in the backward sweep ----
     {
-        const int r = lane < 12 ? lane : 0;
-        const bool act = lane < 12;
+        const int r = (lane < 48) ? (lane >> 2) : 0, part = lane & 3, j0 = 3 * part;
+        const bool wr = lane < 48 && part == 0;
         const int r6 = (r >= 6) ? r - 6 : 0;
         const double sel = (r >= 6) ? 1.0 : 0.0;
-        double nr[12];
+        double nr[3];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) nr[j] = S.st[SO_N + r * 12 + j];
+        for (int q = 0; q < 3; ++q) nr[q] = S.st[SO_N + r * 12 + j0 + q];
         for (int k = 0; k < H; ++k) {
             const ldouble* sl = S.st + k * SK;
             ldouble* xo = (k + 1 < H) ? S.st + (k + 1) * SK + SO_XS : S.xH;
-            double x[12];
+            double x[3];
 #pragma unroll
-            for (int j = 0; j < 12; ++j) x[j] = sl[SO_XS + j];
+            for (int q = 0; q < 3; ++q) x[q] = sl[SO_XS + j0 + q];
             const double n6 = sl[SO_N6 + r6];
-            double nn[12];
-            const ldouble* nxt = S.st + (k + 1 < H ? k + 1 : k) * SK + SO_N + r * 12;
+            double nn[3];
+            const ldouble* nxt = S.st + (k + 1 < H ? k + 1 : k) * SK + SO_N + r * 12 + j0;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) nn[j] = nxt[j];
-            const double a0 = nr[0] * x[0] + nr[1] * x[1] + nr[2] * x[2] + nr[3] * x[3] - sel * n6;
-            const double a1 = nr[4] * x[4] + nr[5] * x[5] + nr[6] * x[6] + nr[7] * x[7];
-            const double a2 = nr[8] * x[8] + nr[9] * x[9] + nr[10] * x[10] + nr[11] * x[11];
-            ldouble* dst = act ? xo + r : S.pa;
-            *dst = a0 + (a1 + a2);
+            for (int q = 0; q < 3; ++q) nn[q] = nxt[q];
+            double v = nr[0] * x[0] + nr[1] * x[1] + nr[2] * x[2];
+            v = quad_sum(v);
+            ldouble* dst = wr ? xo + r : S.pa;
+            *dst = v - sel * n6;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) nr[j] = nn[j];
+            for (int q = 0; q < 3; ++q) nr[q] = nn[q];
             LMPC_SYNC();
         }
     }
