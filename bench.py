@@ -134,6 +134,16 @@ def main():
                       f"oracle over {cores} host threads, {ct:.1f} s wall",
         }
 
+    # HBM bytes per launch of this workload from the committed PMC pass (rocprofv3 FETCH_SIZE + WRITE_SIZE)
+    traffic_bytes = None
+    try:
+        tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        wl = cfg["name"] if args.batch is None else None
+        if wl in tr:
+            traffic_bytes = tr[wl]["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        traffic_bytes = None
+
     if rank == 0:
         line = {
             "metric": "QP solves/sec (Go1, horizon=10, 12 contacts); max GRF err vs exact-QP oracle",
@@ -163,7 +173,7 @@ def main():
                 "peak": roofline.FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / roofline.FP64_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic_bytes,
                 "kernel": "lmpc_qp_kernel",
                 "kernel_ms": kernel_ms,
                 "flop_per_qp": flop_per_qp,
