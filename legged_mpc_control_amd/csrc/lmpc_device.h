@@ -25,12 +25,12 @@ struct DevParams {
 };
 
 // LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
-constexpr int LDS_FIXED_DOUBLES = 988;  // per-QP matrices and buffers
-constexpr int LDS_STAGE_DOUBLES = 358;  // per-stage slot (SK)
+constexpr int LDS_FIXED_DOUBLES = 448;  // per-QP matrices and buffers
+constexpr int LDS_STAGE_DOUBLES = 436;  // per-stage slot (SK)
 inline int lds_doubles(int H) { return LDS_FIXED_DOUBLES + 14 * H + LDS_STAGE_DOUBLES * H; }
 inline size_t lds_bytes(int H) { return (size_t)lds_doubles(H) * sizeof(double); }
-// Global scratch (doubles) per QP: L^-1, V, K, Z per stage (GS in lmpc_kernels.hip, static_asserted).
-constexpr int SCRATCH_STAGE_DOUBLES = 260;
+// Global scratch (doubles) per QP: V, K, Z per stage (GS in lmpc_kernels.hip, static_asserted).
+constexpr int SCRATCH_STAGE_DOUBLES = 182;
 inline size_t scratch_doubles_per_qp(int H) { return (size_t)SCRATCH_STAGE_DOUBLES * H; }
 
 }  // namespace lmpc

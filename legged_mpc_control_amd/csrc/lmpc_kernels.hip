@@ -175,14 +175,14 @@ constexpr int SO_PN = 318;   // 12  p_{k+1}
 constexpr int SO_XS = 330;   // 12  x_k
 constexpr int SO_LAM = 342;  // 12  lambda_{k+1}
 constexpr int SO_ACT = 354;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
-constexpr int SK = 358;
+constexpr int SO_LINV = 358; // 78  L^-1 of Guu, row-packed (LDS-resident: the vector pass reads it twice)
+constexpr int SK = 436;
 // global scratch per stage
-constexpr int GO_LINV = 0;   // 78 packed L^-1 (lower, row-packed)
-constexpr int GO_V = 78;     // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
-constexpr int GO_K = 150;    // 6 x 6 K = V'V
-constexpr int GO_Z = 186;    // 6 x 12 Z = P2_{k+1} A_k
-constexpr int GO_DUMMY = 258;  // sink for the branch-free masked stores
-constexpr int GS = 260;
+constexpr int GO_V = 0;      // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
+constexpr int GO_K = 72;     // 6 x 6 K = V'V
+constexpr int GO_Z = 108;    // 6 x 12 Z = P2_{k+1} A_k
+constexpr int GO_DUMMY = 180;  // sink for the branch-free masked stores
+constexpr int GS = 182;
 
 struct Smem {
     ldouble* G0;   // 72
@@ -190,15 +190,9 @@ struct Smem {
     ldouble* cs;   // 2H
     ldouble* xr;   // 12H
     ldouble* xH;   // 12
-    ldouble* P;    // 144  P_{k+1}
-    ldouble* Pn;   // 144  P_k (double buffer)
-    ldouble* C;    // 72   P22 Bt
-    ldouble* PA6;  // 72   columns 6..11 of P A  (rows 6..11 = columns 6..11 of Z)
     ldouble* GT;   // 144  Guu, column-major
     ldouble* PNL;  // 72   pivot block columns (3 columns x 12 rows), double-buffered
     ldouble* VL;   // 72   V = L^-1 Bt', column-major
-    ldouble* K;    // 36
-    ldouble* KZ;   // 72   K Z of the current stage
     ldouble* pa;   // 12
     ldouble* pb;   // 12
     ldouble* qw;   // 12  state weights q
@@ -206,7 +200,7 @@ struct Smem {
 };
 
 // fixed-size LDS members, in carve order; the total must equal LDS_FIXED_DOUBLES (lmpc_device.h)
-constexpr int LDS_SIZES[] = {72, 40, 12, 144, 144, 72, 72, 144, 72, 72, 36, 72, 12, 12, 12};
+constexpr int LDS_SIZES[] = {72, 40, 12, 144, 72, 72, 12, 12, 12};  // G0 hdr xH GT PNL VL pa pb qw
 constexpr int lds_fixed_sum() {
     int t = 0;
     for (int v : LDS_SIZES) t += v;
@@ -222,15 +216,9 @@ __device__ __forceinline__ Smem carve(double* sm, int H) {
     s.G0 = p; p += 72;
     s.hdr = p; p += 40;
     s.xH = p; p += 12;
-    s.P = p; p += 144;
-    s.Pn = p; p += 144;
-    s.C = p; p += 72;
-    s.PA6 = p; p += 72;
     s.GT = p; p += 144;
     s.PNL = p; p += 72;
     s.VL = p; p += 72;
-    s.K = p; p += 36;
-    s.KZ = p; p += 72;
     s.pa = p; p += 12;
     s.pb = p; p += 12;
     s.qw = p; p += 12;
@@ -446,17 +434,19 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
             par ^= 1;
             SUB(9 + blk);
         }
-        // out, branch-free: lanes 12-17 -> V (LDS + global), lanes 18-29 -> packed L^-1 (upper-triangle
-        // entries and idle lanes go to the stage's dummy slot)
+        // out, branch-free: lanes 12-17 -> V (LDS + global), lanes 18-29 -> packed L^-1 into the stage
+        // slot (upper-triangle entries and idle lanes go to dummy words)
         {
             const bool isv = lane >= 12 && lane < 18, isl = lane >= 18 && lane < 30;
             const int m = isv ? lane - 12 : 0, c = isl ? lane - 18 : 0;
-            ldouble* vl = isv ? S.VL + m * 12 : S.pa;
+            // one LDS destination per lane and row: V -> VL (for K^), L^-1 -> the stage slot, else a dummy word
+            ldouble* vl = S.VL + m * 12;
+            ldouble* li = sl + SO_LINV + c;
 #pragma unroll
             for (int r = 0; r < 12; ++r) {
-                const int gi = isv ? GO_V + m * 12 + r : (isl && r >= c) ? GO_LINV + r * (r + 1) / 2 + c : GO_DUMMY;
-                g[gi] = a[r];
-                vl[isv ? r : 0] = a[r];
+                g[isv ? GO_V + m * 12 + r : GO_DUMMY] = a[r];
+                ldouble* ld = isv ? vl + r : (isl && r >= c) ? li + r * (r + 1) / 2 : S.pb;
+                *ld = a[r];
             }
         }
         LMPC_SYNC();
@@ -544,14 +534,11 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
         k6[i] = ec / 6;
         m6[i] = ec - 6 * k6[i];
     }
-    // ---- prefetch: L^-1 rows, V columns, Z columns ----
-    double li[NT12][12], zc[NT12][6], vc[NT6][12];
+    // ---- prefetch from the global scratch: V columns, Z columns (L^-1 is LDS-resident) ----
+    double zc[NT12][6], vc[NT6][12];
 #pragma unroll
     for (int i = 0; i < NT12; ++i) {
-        const gdouble* Li = gs + k12[i] * GS + GO_LINV + pk(r12[i], 0);  // pk(r, c) < 78 for every c < 12
         const gdouble* Z = gs + k12[i] * GS + GO_Z + r12[i];
-#pragma unroll
-        for (int c = 0; c < 12; ++c) li[i][c] = Li[c];
 #pragma unroll
         for (int m = 0; m < 6; ++m) zc[i][m] = Z[m * 12];
     }
@@ -565,9 +552,10 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
     for (int i = 0; i < NT12; ++i) {
         const ldouble* rr = S.st + k12[i] * SK + SO_RRV;
+        const ldouble* Li = S.st + k12[i] * SK + SO_LINV + pk(r12[i], 0);  // pk(r, c) < 78 for every c < 12
         double v = 0.0;
 #pragma unroll
-        for (int c = 0; c < 12; ++c) v += ((c <= r12[i]) ? li[i][c] : 0.0) * rr[c];
+        for (int c = 0; c < 12; ++c) v += ((c <= r12[i]) ? Li[c] : 0.0) * rr[c];
         if (v12[i]) S.st[k12[i] * SK + SO_RHO + r12[i]] = v;
     }
     LMPC_SYNC();
@@ -645,6 +633,20 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
     if (lane < 12) S.st[SO_XS + lane] = S.hdr[lane];
     LMPC_SYNC();
     SUB(2);
+    // post-pass data from the global scratch, fetched now so that its latency hides behind the forward sweep
+    double zr[NT6][12], vr[NT12][6];
+#pragma unroll
+    for (int i = 0; i < NT6; ++i) {
+        const gdouble* Z = gs + k6[i] * GS + GO_Z + m6[i] * 12;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) zr[i][c] = Z[c];
+    }
+#pragma unroll
+    for (int i = 0; i < NT12; ++i) {
+        const gdouble* V = gs + k12[i] * GS + GO_V + r12[i];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) vr[i][m] = V[m * 12];
+    }
     // ---- forward: x_{k+1} = N_k x_k - [0; n6'_k]; row r split over 4 lanes as in the backward sweep ----
     {
         const int r = (lane < 48) ? (lane >> 2) : 0, part = lane & 3, j0 = 3 * part;
@@ -675,23 +677,6 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
         }
     }
     SUB(3);
-    // post-pass data (fetched after the forward sweep: holding it across the serial loop starves it of registers)
-    double zr[NT6][12], vr[NT12][6], lc[NT12][12];
-#pragma unroll
-    for (int i = 0; i < NT6; ++i) {
-        const gdouble* Z = gs + k6[i] * GS + GO_Z + m6[i] * 12;
-#pragma unroll
-        for (int c = 0; c < 12; ++c) zr[i][c] = Z[c];
-    }
-#pragma unroll
-    for (int i = 0; i < NT12; ++i) {
-        const gdouble* V = gs + k12[i] * GS + GO_V + r12[i];
-        const gdouble* Li = gs + k12[i] * GS + GO_LINV;
-#pragma unroll
-        for (int m = 0; m < 6; ++m) vr[i][m] = V[m * 12];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) lc[i][r] = Li[pk(r, r12[i])];  // in range for every r < 12; masked below
-    }
     // post 1: q2 = Z x_k + v6 + p6   -> SO_N6
 #pragma unroll
     for (int i = 0; i < NT6; ++i) {
@@ -716,9 +701,10 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
     for (int i = 0; i < NT12; ++i) {
         const ldouble* t = S.st + k12[i] * SK + SO_RHO;
+        const ldouble* Li = S.st + k12[i] * SK + SO_LINV;
         double v = 0.0;
 #pragma unroll
-        for (int r = 0; r < 12; ++r) v += ((r >= r12[i]) ? lc[i][r] : 0.0) * t[r];
+        for (int r = 0; r < 12; ++r) v += ((r >= r12[i]) ? Li[pk(r, r12[i])] : 0.0) * t[r];  // pk < 78 for all r
         if (v12[i]) S.st[k12[i] * SK + SO_RRV + r12[i]] = -v;
     }
     LMPC_SYNC();
