@@ -25,8 +25,8 @@ struct DevParams {
 };
 
 // LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
-constexpr int LDS_FIXED_DOUBLES = 448;  // per-QP matrices and buffers
-constexpr int LDS_STAGE_DOUBLES = 436;  // per-stage slot (SK)
+constexpr int LDS_FIXED_DOUBLES = 464;  // per-QP matrices and buffers
+constexpr int LDS_STAGE_DOUBLES = 438;  // per-stage slot (SK)
 inline int lds_doubles(int H) { return LDS_FIXED_DOUBLES + 14 * H + LDS_STAGE_DOUBLES * H; }
 inline size_t lds_bytes(int H) { return (size_t)lds_doubles(H) * sizeof(double); }
 // Global scratch (doubles) per QP: V, K, Z per stage (GS in lmpc_kernels.hip, static_asserted).

@@ -176,7 +176,8 @@ constexpr int SO_XS = 330;   // 12  x_k
 constexpr int SO_LAM = 342;  // 12  lambda_{k+1}
 constexpr int SO_ACT = 354;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
 constexpr int SO_LINV = 358; // 78  L^-1 of Guu, row-packed (LDS-resident: the vector pass reads it twice)
-constexpr int SK = 436;
+constexpr int SO_ZERO = 436; // 2   always 0.0: target of out-of-range operand offsets
+constexpr int SK = 438;
 // global scratch per stage
 constexpr int GO_V = 0;      // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
 constexpr int GO_K = 72;     // 6 x 6 K = V'V
@@ -196,11 +197,12 @@ struct Smem {
     ldouble* pa;   // 12
     ldouble* pb;   // 12
     ldouble* qw;   // 12  state weights q
+    ldouble* zero; // 16  always 0.0
     ldouble* st;   // H * SK
 };
 
 // fixed-size LDS members, in carve order; the total must equal LDS_FIXED_DOUBLES (lmpc_device.h)
-constexpr int LDS_SIZES[] = {72, 40, 12, 144, 72, 72, 12, 12, 12};  // G0 hdr xH GT PNL VL pa pb qw
+constexpr int LDS_SIZES[] = {72, 40, 12, 144, 72, 72, 12, 12, 12, 16};  // G0 hdr xH GT PNL VL pa pb qw zero
 constexpr int lds_fixed_sum() {
     int t = 0;
     for (int v : LDS_SIZES) t += v;
@@ -222,6 +224,7 @@ __device__ __forceinline__ Smem carve(double* sm, int H) {
     s.pa = p; p += 12;
     s.pb = p; p += 12;
     s.qw = p; p += 12;
+    s.zero = p; p += 16;
     s.cs = p; p += 2 * H;
     s.xr = p; p += 12 * H;
     s.st = p;  // offset LDS_FIXED_DOUBLES + 14H doubles (even: 16-B aligned)
@@ -312,6 +315,36 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         P[i] = (r == lc && r < 12) ? S.qw[r < 12 ? r : 0] : 0.0;
     }
     const d4 Qd = P;
+    // ---- lane-static operand maps, hoisted out of the stage loop ----
+    // dt N(yaw) entries of k-blocks 0-1: dt (nc cos + ns sin + n1)
+    double nc[2], ns[2], n1[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int r = 4 * kk + lr, c = lc;
+        nc[kk] = ns[kk] = n1[kk] = 0.0;
+        if (r < 3 && c >= 6 && c < 9) {  // M(yaw)[r][c-6]: [c s 0; -s c 0; 0 0 1]
+            const int j = c - 6;
+            if (r == 0) { nc[kk] = (j == 0) ? dt : 0.0; ns[kk] = (j == 1) ? dt : 0.0; }
+            if (r == 1) { ns[kk] = (j == 0) ? -dt : 0.0; nc[kk] = (j == 1) ? dt : 0.0; }
+            if (r == 2) n1[kk] = (j == 2) ? dt : 0.0;
+        }
+        if (r >= 3 && r < 6 && c == r + 6) n1[kk] = dt;
+    }
+    // B^ (k-blocks 1-2) and Rr operand offsets in the stage slot; out-of-range -> the zero word
+    int boff[2], roff[4];
+#pragma unroll
+    for (int kk = 1; kk < 3; ++kk) {
+        const int r = 4 * kk + lr;
+        boff[kk - 1] = (r >= 6 && r < 12) ? ((lc < 12) ? SO_BT + (r - 6) * 12 + lc : (lc == 12) ? SO_DV + (r - 6) : SO_ZERO)
+                                          : SO_ZERO;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        roff[i] = (r < 12 && lc < 12 && (r / 3) == (lc / 3)) ? SO_RR + (r / 3) * 9 + (r % 3) * 3 + (lc % 3) : SO_ZERO;
+    }
+    // K^ operand: column lc-6 of V for lc in 6-11, else the zero block
+    const ldouble* vop = (lc >= 6 && lc < 12) ? S.VL + (lc - 6) * 12 + lr : S.zero;
     SUB_DECL
     for (int k = H - 1; k >= 0; --k) {
         const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
@@ -321,15 +354,9 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         // ---- operands: dt N(yaw) (k-blocks 0-1: rows 0-7) and B^ (k-blocks 1-2) ----
         double nh[2], bh[2];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) nh[kk] = dtN_entry(4 * kk + lr, lc, ck, sk, dt);
-#pragma unroll
-        for (int kk = 1; kk < 3; ++kk) {
-            const int r = 4 * kk + lr;  // row of B^; rows 6-11 = Bt rows 0-5
-            const int m = (r >= 6 && r < 12) ? r - 6 : 0;
-            const double vb = Bt[m * 12 + (lc < 12 ? lc : 0)];
-            const double vd = sl[SO_DV + m];
-            bh[kk - 1] = (r >= 6 && r < 12) ? ((lc < 12) ? vb : (lc == 12) ? vd : 0.0) : 0.0;
-        }
+        for (int kk = 0; kk < 2; ++kk) nh[kk] = fma(nc[kk], ck, fma(ns[kk], sk, n1[kk]));
+        bh[0] = sl[boff[0]];
+        bh[1] = sl[boff[1]];
         // ---- C^ = P B^ ; PA = P A_k = P + P (dt N) ----
         d4 C = {0.0, 0.0, 0.0, 0.0};
         C = MFMA64(P[1], bh[0], C);
@@ -340,13 +367,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         // ---- Guu = Rr + B^' C^ (Rr: 3x3 leg blocks on the diagonal) ----
         d4 G;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = lr + 4 * i;
-            const bool on = r < 12 && lc < 12 && (r / 3) == (lc / 3);
-            const int rr = r < 12 ? r : 0, cc = lc < 12 ? lc : 0;
-            const double v = sl[SO_RR + (rr / 3) * 9 + (rr % 3) * 3 + (cc % 3)];
-            G[i] = on ? v : 0.0;
-        }
+        for (int i = 0; i < 4; ++i) G[i] = sl[roff[i]];
         G = MFMA64(bh[0], C[1], G);
         G = MFMA64(bh[1], C[2], G);
         // ---- out: v = C^[:, 12], Guu column-major for the elimination, Z = rows 6-11 of PA ----
@@ -453,15 +474,10 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         SUB(7);
         // ---- K^ = V^' V^ (V^ = [0 | V], columns 6-11) ----
         d4 KH = {0.0, 0.0, 0.0, 0.0};
-        {
-            const bool vc = lc >= 6 && lc < 12;
-            const int m = vc ? lc - 6 : 0;
 #pragma unroll
-            for (int kk = 0; kk < 3; ++kk) {
-                const double v = S.VL[m * 12 + 4 * kk + lr];
-                const double vh = vc ? v : 0.0;
-                KH = MFMA64(vh, vh, KH);
-            }
+        for (int kk = 0; kk < 3; ++kk) {
+            const double vh = vop[4 * kk];
+            KH = MFMA64(vh, vh, KH);
         }
         // ---- KZ^ = K^ PA (k-blocks 1-2: K^ is zero outside rows/columns 6-11) ----
         d4 KZ = {0.0, 0.0, 0.0, 0.0};
@@ -1012,6 +1028,8 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         S.G0[e] = v;
     }
     if (lane < 12) S.qw[lane] = prm.q[lane];
+    if (lane < 16) S.zero[lane] = 0.0;
+    for (int k = lane; k < H; k += 64) S.st[k * SK + SO_ZERO] = S.st[k * SK + SO_ZERO + 1] = 0.0;
     LMPC_SYNC();
 
     // ---- leg-step ownership and IPM state ----
