@@ -101,7 +101,8 @@ def main():
     it = d_it.cpu().numpy()
     ipm_mean = float(np.mean(it & 0xFFFF))
     pol_mean = float(np.mean(it >> 16))
-    flop_per_qp = roofline.qp_flop(H, ipm_mean, pol_mean)
+    flop_per_qp = roofline.survey_flop(H, ipm_mean, pol_mean)  # SURVEY.md 8(d) contract figure
+    riccati_flop_per_qp = roofline.qp_flop(H, ipm_mean, pol_mean)  # the build's own useful-flop count
     achieved_tf = flop_per_qp * B / (kernel_ms * 1e-3) / 1e12
     global_batch = cfg["batch"] if strong else B * world
     total_qps = global_batch * args.steps / t_max
@@ -177,6 +178,8 @@ def main():
                 "kernel": "lmpc_qp_kernel",
                 "kernel_ms": kernel_ms,
                 "flop_per_qp": flop_per_qp,
+                "flop_model": "SURVEY.md 8(d): F0 + K*F_iter + rounds*(N^3/3 + 2N^2), K/rounds = measured means",
+                "riccati_flop_per_qp": riccati_flop_per_qp,
                 "hbm_gbs": roofline.qp_bytes(H) * B / (kernel_ms * 1e-3) / 1e9,
             },
             "cpu_baseline": cpu,

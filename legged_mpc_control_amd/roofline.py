@@ -1,7 +1,18 @@
-"""Algorithmic work model of the fused QP kernel (used by bench.py's roofline).
+"""Algorithmic work models of the QP path (used by bench.py's roofline).
 
-Counts are the useful fp64 flops of the algorithm (FMA = 2 flops), per horizon
-stage, derived from lmpc_kernels.hip (DESIGN.md "Roofline" explains each term):
+`survey_flop` is the contract figure for `roofline.achieved`: SURVEY.md 8(d)'s algorithmic
+flops of one QP of horizon H, independent of how the build solves it --
+
+  N = 12H, block GEMM cost c = 2 * 12^3
+  F0     = c (H(H-1)/2 + H) + c H(H+1)(H+2)/6 + (N^2 + 288 H) + N^3/3   (condensation + factorisation)
+  F_iter = 2 N^2 + 144 H                                            (per iteration)
+  F      = F0 + K * F_iter + rounds * (N^3/3 + 2 N^2)                (polish: refactor + solve)
+
+with K the measured mean interior-point iterations and `rounds` the mean polish rounds.
+F0 = 1.544M / 10.72M / 34.44M flop at H = 10 / 20 / 30.
+
+`qp_flop` is the build's own count of useful fp64 flops of its Riccati formulation (FMA = 2
+flops), per horizon stage, reported beside it:
 
   Riccati factorisation stage (riccati_factor):
     Bt = G0 T (216 FMA) + G0 up (72) + PB = P[:,6:12] Bt (864) + v = P d (72)
@@ -36,6 +47,27 @@ def polish_round_flop(H: int) -> int:
 def qp_flop(H: int, ipm_iters: float, polish_rounds: float) -> float:
     """Algorithmic flops of one QP given its (mean) IPM iterations and polish rounds."""
     return ipm_iters * ipm_iter_flop(H) + polish_rounds * polish_round_flop(H)
+
+
+def survey_f0(H: int) -> float:
+    N = 12 * H
+    c = 2 * 12 ** 3
+    f_pred = c * (H * (H - 1) / 2 + H)
+    f_hess = c * H * (H + 1) * (H + 2) / 6
+    f_grad = N * N + 288 * H
+    f_chol = N ** 3 / 3
+    return f_pred + f_hess + f_grad + f_chol
+
+
+def survey_f_iter(H: int) -> float:
+    N = 12 * H
+    return 2 * N * N + 144 * H
+
+
+def survey_flop(H: int, iters: float, polish_rounds: float) -> float:
+    """SURVEY.md 8(d) algorithmic flops of one QP (the contract figure for roofline.achieved)."""
+    N = 12 * H
+    return survey_f0(H) + iters * survey_f_iter(H) + polish_rounds * (N ** 3 / 3 + 2 * N * N)
 
 
 def qp_bytes(H: int) -> int:
