@@ -35,6 +35,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="QPs per GPU (default: config batch; config 4: 65536/N)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall seconds)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--flat", action="store_true", help="config 4 without its terrain normals (reference problem)")
     return ap.parse_args()
 
 
@@ -66,10 +67,13 @@ def main():
         B = args.batch if args.batch is not None else cfg["batch"]
         first, _ = D.shard_range(rank, world, B)
     p, H, rec, con = synth.config_batch(args.config, count=B, first_index=first)
+    nrm = None if args.flat else synth.config_normals(args.config, count=B, first_index=first)  # config 4 terrain
+    wl_name = cfg["name"] + ("+terrain" if nrm is not None else "")
 
     solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank)
     d_rec = torch.from_numpy(rec).to(dev)
     d_con = torch.from_numpy(con).to(dev)
+    d_nrm = None if nrm is None else torch.from_numpy(nrm).to(dev)
     d_grf = torch.empty((B, H, 12), dtype=torch.float64, device=dev)
     d_st = torch.empty(B, dtype=torch.int32, device=dev)
     d_it = torch.empty(B, dtype=torch.int32, device=dev)
@@ -77,7 +81,7 @@ def main():
     torch.cuda.set_stream(stream)
 
     for _ in range(args.warmup):
-        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream)
+        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream, normals=d_nrm)
     torch.cuda.synchronize(dev)
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -87,7 +91,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream)
+        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream, normals=d_nrm)
         evs[i][1].record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
@@ -116,12 +120,12 @@ def main():
 
         op = O.params_from(p)
         cores = min(16, os.cpu_count() or 1)
-        ref, ost, _ = O.solve_batch(op, H, rec, con, n_threads=cores)  # warm + parity reference
+        ref, ost, _ = O.solve_batch(op, H, rec, con, n_threads=cores, normals=nrm)  # warm + parity reference
         max_err = float(np.max(np.abs(grf - ref) / np.maximum(1.0, np.abs(ref))))
         reps = 0
         t1 = time.perf_counter()
         while True:
-            O.solve_batch(op, H, rec, con, n_threads=cores)
+            O.solve_batch(op, H, rec, con, n_threads=cores, normals=nrm)
             reps += 1
             if time.perf_counter() - t1 >= args.cpu_seconds:
                 break
@@ -131,7 +135,7 @@ def main():
             "unit": "QP/s",
             "cores": cores,
             "kind": "port",
-            "sample": f"{reps} x the rank-0 batch ({B} QPs, {cfg['name']}), fp64 dense Goldfarb-Idnani "
+            "sample": f"{reps} x the rank-0 batch ({B} QPs, {wl_name}), fp64 dense Goldfarb-Idnani "
                       f"oracle over {cores} host threads, {ct:.1f} s wall",
         }
 
@@ -139,7 +143,7 @@ def main():
     traffic_bytes = None
     try:
         tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-        wl = cfg["name"] if args.batch is None else None
+        wl = wl_name if args.batch is None else None
         if wl in tr:
             traffic_bytes = tr[wl]["bytes_per_launch"]
     except (OSError, ValueError, KeyError):
@@ -160,12 +164,13 @@ def main():
             "dtype": "f64",
             "data": "synthetic (Philox-seeded perturbed states, SURVEY.md 8d)",
             "config": {
-                "workload": cfg["name"] if args.batch is None else f"{cfg['name']}@b{B}",
+                "workload": wl_name if args.batch is None else f"{wl_name}@b{B}",
                 "horizon": H,
                 "batch_per_gpu": B,
                 "global_batch": global_batch,
                 "robot": cfg["robot"],
                 "gait": "mixed" if cfg["gait"] < 0 else ["trot", "crawl", "trot_with_stand", "stand"][cfg["gait"]],
+                "terrain": None if nrm is None else f"per-leg normals, tilt U(0, {synth.TERRAIN_THETA_MAX}) rad",
                 "parallelism": f"dp{world} (independent QP shards, no collective)",
             },
             "roofline": {

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LMPC_ABI_VERSION 1
+#define LMPC_ABI_VERSION 2 /* 2: terrain-normal extension (_ex entry points) */
 #define LMPC_MAX_HORIZON 32
 
 /* return codes (API level) */
@@ -128,6 +128,26 @@ int lmpc_solve_batch_device(lmpc_ctx* ctx, const double* d_rec, const uint8_t* d
 /* Synchronise the context's stream. */
 int lmpc_sync(lmpc_ctx* ctx);
 
+/* ---- terrain extension (ABI 2) -------------
+ * Beyond the reference, which is flat-ground only (ConvexQPSolver.cpp:131-172).
+ * normals[batch][4][3]: per-instance, per-leg ground normal (FL,FR,RL,RR; need
+ * not be unit length; n_z > 0), constant over the horizon.  The reference's
+ * friction pyramid and 0 <= f_n <= f_max*contact bound then act on the
+ * contact-frame force g = R'f, R = lmpc_terrain_frame(n): columns t1, t2, n, the
+ * minimal rotation taking e_z to n.  n = e_z gives R = I exactly, so flat
+ * normals pose the reference's problem and agree with lmpc_solve_batch to
+ * rounding; normals == NULL is the flat (reference) problem itself.  GRFs are
+ * returned in the world frame, as always. */
+void lmpc_terrain_frame(const double normal[3], double R[9] /* row-major */);
+/* host buffers; returns LMPC_ERR_ARG if some normal has n_z <= 0 or is not finite */
+int lmpc_solve_batch_ex(lmpc_ctx* ctx, const double* rec, const uint8_t* contact,
+                        const double* normals, int batch, double* grf, int32_t* status,
+                        int32_t* iters);
+/* device buffers, asynchronous (normals unchecked: the caller guarantees n_z > 0) */
+int lmpc_solve_batch_device_ex(lmpc_ctx* ctx, const double* d_rec, const uint8_t* d_contact,
+                               const double* d_normals, int batch, double* d_grf,
+                               int32_t* d_status, int32_t* d_iters, void* stream);
+
 /* ---- host-side path helpers (exact restatements of the reference) ------ */
 
 /* LeggedContactFSM gait tables (LeggedContactFSM.cpp:93-212). */
@@ -176,6 +196,12 @@ void lmpc_synth_cfg_a1_standing(lmpc_synth_cfg* c);
 /* Instance b of the batch is global index first_index+b; identical on every rank. */
 int lmpc_synth_fill(const lmpc_params* p, const lmpc_synth_cfg* cfg, int horizon, uint64_t seed,
                     int64_t first_index, int count, double* rec, uint8_t* contact);
+/* Terrain normals for instances first_index..first_index+count-1 (config 4):
+ * per leg, tilt theta ~ U(0, theta_max) about a direction phi ~ U(-pi, pi),
+ * n = (sin theta cos phi, sin theta sin phi, cos theta).  A Philox stream separate
+ * from lmpc_synth_fill's, so records are identical with and without normals. */
+int lmpc_synth_normals(uint64_t seed, int64_t first_index, int count, double theta_max,
+                       double* normals /* [count][4][3] */);
 
 #ifdef __cplusplus
 }

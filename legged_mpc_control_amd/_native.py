@@ -26,7 +26,10 @@ EXPORTED_SYMBOLS = (
     "lmpc_set_params", "lmpc_reserve", "lmpc_solve_batch", "lmpc_solve_batch_device", "lmpc_sync",
     "lmpc_predict_contact", "lmpc_current_contact", "lmpc_contact_schedule", "lmpc_pack_record",
     "lmpc_synth_cfg_go1", "lmpc_synth_cfg_a1_standing", "lmpc_synth_fill",
+    # ABI 2: terrain extension
+    "lmpc_terrain_frame", "lmpc_solve_batch_ex", "lmpc_solve_batch_device_ex", "lmpc_synth_normals",
 )
+ABI_VERSION = 2
 
 
 class LmpcParams(ctypes.Structure):
@@ -136,7 +139,15 @@ def lib():
         L.lmpc_synth_fill.argtypes = [pp, ctypes.POINTER(LmpcSynthCfg), ctypes.c_int, ctypes.c_uint64,
                                       ctypes.c_int64, ctypes.c_int, dp, u8p]
         L.lmpc_synth_fill.restype = ctypes.c_int
-        if L.lmpc_abi_version() != 1:
+        L.lmpc_terrain_frame.argtypes = [dp, dp]
+        L.lmpc_terrain_frame.restype = None
+        L.lmpc_solve_batch_ex.argtypes = [vp, dp, u8p, dp, ctypes.c_int, dp, i32p, i32p]
+        L.lmpc_solve_batch_ex.restype = ctypes.c_int
+        L.lmpc_solve_batch_device_ex.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
+        L.lmpc_solve_batch_device_ex.restype = ctypes.c_int
+        L.lmpc_synth_normals.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_double, dp]
+        L.lmpc_synth_normals.restype = ctypes.c_int
+        if L.lmpc_abi_version() != ABI_VERSION:
             raise NativeLibraryError("liblmpc.so ABI version mismatch")
         _lib = L
         return L

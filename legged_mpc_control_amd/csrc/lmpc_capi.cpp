@@ -6,6 +6,7 @@
 // their host buffers; nothing is retained after a call returns.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstring>
 #include <new>
 
@@ -13,8 +14,8 @@
 #include "lmpc_device.h"
 
 namespace lmpc {
-hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, int batch, double* grf,
-                     int32_t* status, int32_t* iters, double* scratch, hipStream_t stream);
+hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                     int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, hipStream_t stream);
 }
 
 struct lmpc_ctx {
@@ -25,6 +26,7 @@ struct lmpc_ctx {
     hipStream_t stream = nullptr;
     double* d_rec = nullptr;
     uint8_t* d_contact = nullptr;
+    double* d_normals = nullptr;  // terrain staging (host _ex path)
     double* d_grf = nullptr;
     int32_t* d_status = nullptr;
     int32_t* d_iters = nullptr;
@@ -67,6 +69,7 @@ bool params_ok(const lmpc_params* p) {
 void free_bufs(lmpc_ctx* c) {
     (void)hipFree(c->d_rec);
     (void)hipFree(c->d_contact);
+    (void)hipFree(c->d_normals);
     (void)hipFree(c->d_grf);
     (void)hipFree(c->d_status);
     (void)hipFree(c->d_iters);
@@ -75,6 +78,7 @@ void free_bufs(lmpc_ctx* c) {
     c->scratch_qps = 0;
     c->d_rec = nullptr;
     c->d_contact = nullptr;
+    c->d_normals = nullptr;
     c->d_grf = nullptr;
     c->d_status = nullptr;
     c->d_iters = nullptr;
@@ -108,6 +112,7 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
         const size_t rl = (size_t)lmpc_record_len(horizon);
         bool ok = hipMalloc(&c->d_rec, (size_t)max_batch * rl * sizeof(double)) == hipSuccess &&
                   hipMalloc(&c->d_contact, (size_t)max_batch * 4 * horizon) == hipSuccess &&
+                  hipMalloc(&c->d_normals, (size_t)max_batch * 12 * sizeof(double)) == hipSuccess &&
                   hipMalloc(&c->d_grf, (size_t)max_batch * 12 * horizon * sizeof(double)) == hipSuccess &&
                   hipMalloc(&c->d_status, (size_t)max_batch * sizeof(int32_t)) == hipSuccess &&
                   hipMalloc(&c->d_iters, (size_t)max_batch * sizeof(int32_t)) == hipSuccess;
@@ -170,8 +175,8 @@ int lmpc_reserve(lmpc_ctx* c, int batch) {
     return LMPC_OK;
 }
 
-int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, int batch, double* d_grf,
-                            int32_t* d_status, int32_t* d_iters, void* stream) {
+int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, const double* d_normals,
+                               int batch, double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_rec || !d_contact || !d_grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -179,22 +184,38 @@ int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_c
         const int rc = lmpc_reserve(c, batch);
         if (rc != LMPC_OK) return rc;
     }
-    const hipError_t e = lmpc::launch_qp(c->prm, d_rec, d_contact, batch, d_grf, d_status, d_iters, c->d_scratch, s);
+    const hipError_t e =
+        lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
 }
 
-int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int batch, double* grf,
-                     int32_t* status, int32_t* iters) {
+int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, int batch, double* d_grf,
+                            int32_t* d_status, int32_t* d_iters, void* stream) {
+    return lmpc_solve_batch_device_ex(c, d_rec, d_contact, nullptr, batch, d_grf, d_status, d_iters, stream);
+}
+
+int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, const double* normals, int batch,
+                        double* grf, int32_t* status, int32_t* iters) {
     if (!c || batch < 0 || batch > c->max_batch || (batch > 0 && (!rec || !contact || !grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
+    if (normals)
+        for (size_t i = 0; i < (size_t)batch * 4; ++i) {
+            const double* n = normals + 3 * i;
+            if (!(n[2] > 0.0) || !std::isfinite(n[0]) || !std::isfinite(n[1]) || !std::isfinite(n[2]))
+                return LMPC_ERR_ARG;
+        }
     if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
     const size_t rl = (size_t)lmpc_record_len(c->H);
     hipStream_t s = c->stream;
     if (hipMemcpyAsync(c->d_rec, rec, (size_t)batch * rl * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(c->d_contact, contact, (size_t)batch * 4 * c->H, hipMemcpyHostToDevice, s) != hipSuccess)
         return LMPC_ERR_DEVICE;
-    int rc = lmpc_solve_batch_device(c, c->d_rec, c->d_contact, batch, c->d_grf, c->d_status, c->d_iters, s);
+    if (normals && hipMemcpyAsync(c->d_normals, normals, (size_t)batch * 12 * sizeof(double), hipMemcpyHostToDevice,
+                                  s) != hipSuccess)
+        return LMPC_ERR_DEVICE;
+    int rc = lmpc_solve_batch_device_ex(c, c->d_rec, c->d_contact, normals ? c->d_normals : nullptr, batch, c->d_grf,
+                                        c->d_status, c->d_iters, s);
     if (rc != LMPC_OK) return rc;
     if (hipMemcpyAsync(grf, c->d_grf, (size_t)batch * 12 * c->H * sizeof(double), hipMemcpyDeviceToHost, s) !=
         hipSuccess)
@@ -206,6 +227,11 @@ int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int
                      hipSuccess)
         return LMPC_ERR_DEVICE;
     return hipStreamSynchronize(s) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
+}
+
+int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int batch, double* grf,
+                     int32_t* status, int32_t* iters) {
+    return lmpc_solve_batch_ex(c, rec, contact, nullptr, batch, grf, status, iters);
 }
 
 int lmpc_sync(lmpc_ctx* c) {

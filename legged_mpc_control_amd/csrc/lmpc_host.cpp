@@ -53,13 +53,13 @@ struct Philox {
     uint32_t out[4];
     int used;
 
-    Philox(uint64_t seed, uint64_t index) {
+    Philox(uint64_t seed, uint64_t index, uint32_t stream = 0x4c4d5043u /* "LMPC" */) {
         key[0] = (uint32_t)seed;
         key[1] = (uint32_t)(seed >> 32);
         ctr[0] = (uint32_t)index;
         ctr[1] = (uint32_t)(index >> 32);
         ctr[2] = 0;
-        ctr[3] = 0x4c4d5043u;  // "LMPC"
+        ctr[3] = stream;
         used = 4;
     }
     void block() {
@@ -295,6 +295,32 @@ int lmpc_synth_fill(const lmpc_params* p, const lmpc_synth_cfg* cfg, int horizon
         lmpc_pack_record(p, horizon, &st, r, nullptr);
         lmpc_contact_schedule(gait, phase, cfg->gait_speed, p->dt, horizon, plan,
                               contact + (size_t)b * 4 * horizon);
+    }
+    return LMPC_OK;
+}
+
+void lmpc_terrain_frame(const double nin[3], double R[9]) {
+    // minimal rotation e_z -> n (Rodrigues about e_z x n, closed form); n = e_z gives I exactly
+    const double nn = std::sqrt(nin[0] * nin[0] + nin[1] * nin[1] + nin[2] * nin[2]);
+    const double nx = nin[0] / nn, ny = nin[1] / nn, c = nin[2] / nn;
+    const double h = 1.0 / (1.0 + c);
+    R[0] = 1.0 - nx * nx * h; R[1] = -nx * ny * h;      R[2] = nx;
+    R[3] = -nx * ny * h;      R[4] = 1.0 - ny * ny * h; R[5] = ny;
+    R[6] = -nx;               R[7] = -ny;               R[8] = c;
+}
+
+int lmpc_synth_normals(uint64_t seed, int64_t first_index, int count, double theta_max, double* normals) {
+    if (!normals || count < 0 || !(theta_max >= 0.0) || theta_max >= 1.5707963267948966) return LMPC_ERR_ARG;
+    for (int b = 0; b < count; ++b) {
+        Philox rng(seed, (uint64_t)(first_index + b), 0x54455252u /* "TERR" */);
+        for (int j = 0; j < 4; ++j) {
+            const double th = rng.uniform(0.0, theta_max);
+            const double ph = rng.uniform(-M_PI, M_PI);
+            double* n = normals + (size_t)b * 12 + 3 * j;
+            n[0] = std::sin(th) * std::cos(ph);
+            n[1] = std::sin(th) * std::sin(ph);
+            n[2] = std::cos(th);
+        }
     }
     return LMPC_OK;
 }

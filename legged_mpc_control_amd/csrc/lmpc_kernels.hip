@@ -956,10 +956,16 @@ __device__ __forceinline__ void leg_u(const Smem& S, const bool (&valid)[LS], co
 
 // ---------------------------------------------------------------------------
 // The fused per-QP kernel.  LS = leg-steps owned per lane = ceil(4H / 64).
+//
+// TERRAIN (extension): each leg's force variable is its contact-frame force
+// g = R_j'f (R_j = terrain_frame(n_j)), so the reference's pyramid/bound code below runs
+// unchanged on g.  What changes: the input matrix G0 -> G0 blkdiag(R_j), the input Hessian
+// block diag(r_j) -> R_j' diag(r_j) R_j, and the output f = R_j g.  R_j = I for n_j = e_z.
 // ---------------------------------------------------------------------------
-template <int LS>
+template <int LS, bool TERRAIN>
 __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const double* __restrict__ rec,
-                                                     const uint8_t* __restrict__ contact, int batch,
+                                                     const uint8_t* __restrict__ contact,
+                                                     const double* __restrict__ normals, int batch,
                                                      double* __restrict__ grf, int32_t* __restrict__ status,
                                                      int32_t* __restrict__ iters, double* __restrict__ scratch) {
     extern __shared__ __attribute__((aligned(16))) double lmpc_smem[];
@@ -969,6 +975,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     const int H = prm.H;
     const int RL = 33 + 12 * H;
     const Smem S = carve(lmpc_smem, H);
+    ldouble* const tf = S.st + SK * H;  // TERRAIN only: R_j (9 each, row-major) | R_j' diag(r_j) R_j packed (6 each)
     double* gs = scratch + (size_t)qp * GS * H;
     const double mu = prm.mu, fzmax = prm.fmax, dt = prm.dt;
     STAMP_DECL
@@ -979,6 +986,26 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
         const double v = rin[i];
         if (i < 33) S.hdr[i] = v;
         else S.xr[i - 33] = v;
+    }
+    if constexpr (TERRAIN) {
+        if (lane < 4) {
+            // contact frame of leg `lane` (same closed form as lmpc_terrain_frame, lmpc_host.cpp)
+            const double* nin = normals + (size_t)qp * 12 + 3 * lane;
+            const double n0 = nin[0], n1 = nin[1], n2 = nin[2];
+            const double nn = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+            const double nx = n0 / nn, ny = n1 / nn, c = n2 / nn;
+            const double h = 1.0 / (1.0 + c);
+            const double R[9] = {1.0 - nx * nx * h, -nx * ny * h, nx, -nx * ny * h, 1.0 - ny * ny * h, ny, -nx, -ny, c};
+#pragma unroll
+            for (int e = 0; e < 9; ++e) tf[9 * lane + e] = R[e];
+            const double r0 = prm.r[3 * lane], r1 = prm.r[3 * lane + 1], r2 = prm.r[3 * lane + 2];
+            int e = 0;
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = a; b < 3; ++b)  // packed [xx xy xz yy yz zz]
+                    tf[36 + 6 * lane + e++] = r0 * R[a] * R[b] + r1 * R[3 + a] * R[3 + b] + r2 * R[6 + a] * R[6 + b];
+        }
     }
     LMPC_SYNC();
     double iw[9];  // (R I_b R')^-1, computed redundantly by every lane
@@ -1015,15 +1042,30 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     for (int e = lane; e < 72; e += 64) {
         const int r = e / 12, c = e % 12, j = c / 3, cc = c % 3;
         double v;
-        if (r < 3) {
-            const ldouble* ft = S.hdr + LMPC_REC_FEET + 3 * j;
-            double sk[3];  // column cc of skew(ft)
-            if (cc == 0) { sk[0] = 0.0; sk[1] = ft[2]; sk[2] = -ft[1]; }
-            else if (cc == 1) { sk[0] = -ft[2]; sk[1] = 0.0; sk[2] = ft[0]; }
-            else { sk[0] = ft[1]; sk[1] = -ft[0]; sk[2] = 0.0; }
-            v = dt * (iw[r * 3 + 0] * sk[0] + iw[r * 3 + 1] * sk[1] + iw[r * 3 + 2] * sk[2]);
+        if constexpr (!TERRAIN) {
+            if (r < 3) {
+                const ldouble* ft = S.hdr + LMPC_REC_FEET + 3 * j;
+                double sk[3];  // column cc of skew(ft)
+                if (cc == 0) { sk[0] = 0.0; sk[1] = ft[2]; sk[2] = -ft[1]; }
+                else if (cc == 1) { sk[0] = -ft[2]; sk[1] = 0.0; sk[2] = ft[0]; }
+                else { sk[0] = ft[1]; sk[1] = -ft[0]; sk[2] = 0.0; }
+                v = dt * (iw[r * 3 + 0] * sk[0] + iw[r * 3 + 1] * sk[1] + iw[r * 3 + 2] * sk[2]);
+            } else {
+                v = (r - 3 == cc) ? dt / prm.mass : 0.0;
+            }
         } else {
-            v = (r - 3 == cc) ? dt / prm.mass : 0.0;
+            // (G0 R_j)[r][cc] = sum_p G0[r][3j+p] R_j[p][cc]
+            const ldouble* Rj = tf + 9 * j;
+            if (r < 3) {
+                const ldouble* ft = S.hdr + LMPC_REC_FEET + 3 * j;
+                // row r of dt I_w^-1 skew(ft): w_p = dt (iw[r,:] . skew column p)
+                const double w0 = dt * (iw[r * 3 + 1] * ft[2] - iw[r * 3 + 2] * ft[1]);
+                const double w1 = dt * (-iw[r * 3 + 0] * ft[2] + iw[r * 3 + 2] * ft[0]);
+                const double w2 = dt * (iw[r * 3 + 0] * ft[1] - iw[r * 3 + 1] * ft[0]);
+                v = w0 * Rj[cc] + w1 * Rj[3 + cc] + w2 * Rj[6 + cc];
+            } else {
+                v = (dt / prm.mass) * Rj[3 * (r - 3) + cc];
+            }
         }
         S.G0[e] = v;
     }
@@ -1122,12 +1164,22 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                         }
                         const double sx = W[0] + W[1], sy = W[2] + W[3];
                         const int j = lsj[t];
-                        Rt[t][0] = prm.r[3 * j + 0] + sx;
-                        Rt[t][1] = 0.0;
-                        Rt[t][2] = mu * (W[0] - W[1]);
-                        Rt[t][3] = prm.r[3 * j + 1] + sy;
-                        Rt[t][4] = mu * (W[2] - W[3]);
-                        Rt[t][5] = prm.r[3 * j + 2] + mu * mu * (sx + sy) + W[4];
+                        if constexpr (!TERRAIN) {
+                            Rt[t][0] = prm.r[3 * j + 0] + sx;
+                            Rt[t][1] = 0.0;
+                            Rt[t][2] = mu * (W[0] - W[1]);
+                            Rt[t][3] = prm.r[3 * j + 1] + sy;
+                            Rt[t][4] = mu * (W[2] - W[3]);
+                            Rt[t][5] = prm.r[3 * j + 2] + mu * mu * (sx + sy) + W[4];
+                        } else {
+                            const ldouble* rb = tf + 36 + 6 * j;
+                            Rt[t][0] = rb[0] + sx;
+                            Rt[t][1] = rb[1];
+                            Rt[t][2] = rb[2] + mu * (W[0] - W[1]);
+                            Rt[t][3] = rb[3] + sy;
+                            Rt[t][4] = rb[4] + mu * (W[2] - W[3]);
+                            Rt[t][5] = rb[5] + mu * mu * (sx + sy) + W[4];
+                        }
                         cons_tw(wv, mu, rt[t]);
                     }
                 }
@@ -1145,11 +1197,16 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                         up[t][0] = up[t][1] = up[t][2] = 0.0;
                     }
                     const int j = lsj[t];
-                    Rt[t][0] = prm.r[3 * j];
-                    Rt[t][1] = Rt[t][2] = 0.0;
-                    Rt[t][3] = prm.r[3 * j + 1];
-                    Rt[t][4] = 0.0;
-                    Rt[t][5] = prm.r[3 * j + 2];
+                    if constexpr (!TERRAIN) {
+                        Rt[t][0] = prm.r[3 * j];
+                        Rt[t][1] = Rt[t][2] = 0.0;
+                        Rt[t][3] = prm.r[3 * j + 1];
+                        Rt[t][4] = 0.0;
+                        Rt[t][5] = prm.r[3 * j + 2];
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 6; ++e) Rt[t][e] = tf[36 + 6 * j + e];
+                    }
                     rt[t][0] = rt[t][1] = rt[t][2] = 0.0;
                 }
             }
@@ -1268,9 +1325,19 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                     if (!valid[t]) continue;
                     const int k = lsk[t], j = lsj[t];
                     const ldouble* lam = S.st + k * SK + SO_LAM;
+                    double ru[3];  // input-Hessian block times u
+                    if constexpr (!TERRAIN) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) ru[p] = prm.r[3 * j + p] * u[t][p];
+                    } else {
+                        const ldouble* rb = tf + 36 + 6 * j;
+                        ru[0] = rb[0] * u[t][0] + rb[1] * u[t][1] + rb[2] * u[t][2];
+                        ru[1] = rb[1] * u[t][0] + rb[3] * u[t][1] + rb[4] * u[t][2];
+                        ru[2] = rb[2] * u[t][0] + rb[4] * u[t][1] + rb[5] * u[t][2];
+                    }
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
-                        double v = prm.r[3 * j + p] * u[t][p];
+                        double v = ru[p];
 #pragma unroll
                         for (int m = 0; m < 6; ++m) v += S.G0[m * 12 + 3 * j + p] * lam[6 + m];
                         g[t][p] = v;
@@ -1380,8 +1447,14 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     for (int t = 0; t < LS; ++t) {
         if (!valid[t]) continue;
         const int ls = lane + 64 * t;
+        double fo[3] = {u[t][0], u[t][1], u[t][2]};
+        if constexpr (TERRAIN) {  // f = R_j g (world frame)
+            const ldouble* Rj = tf + 9 * lsj[t];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) gout[3 * ls + p] = (anybad || !st[t]) ? 0.0 : u[t][p];
+            for (int p = 0; p < 3; ++p) fo[p] = Rj[3 * p] * u[t][0] + Rj[3 * p + 1] * u[t][1] + Rj[3 * p + 2] * u[t][2];
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) gout[3 * ls + p] = (anybad || !st[t]) ? 0.0 : fo[p];
     }
     STAMP(5);  // epilogue
     STAMP_FLUSH(qp);
@@ -1391,24 +1464,37 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     }
 }
 
-template __global__ void lmpc_qp_kernel<1>(const DevParams, const double*, const uint8_t*, int, double*, int32_t*,
-                                           int32_t*, double*);
-template __global__ void lmpc_qp_kernel<2>(const DevParams, const double*, const uint8_t*, int, double*, int32_t*,
-                                           int32_t*, double*);
+#define LMPC_INST(LS_, T_)                                                                                      \
+    template __global__ void lmpc_qp_kernel<LS_, T_>(const DevParams, const double*, const uint8_t*, const double*, \
+                                                     int, double*, int32_t*, int32_t*, double*);
+LMPC_INST(1, false)
+LMPC_INST(2, false)
+LMPC_INST(1, true)
+LMPC_INST(2, true)
+#undef LMPC_INST
 
-// Host-side launcher (called from lmpc_capi.cpp).
-hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, int batch, double* grf,
-                     int32_t* status, int32_t* iters, double* scratch, hipStream_t stream) {
-    const size_t lds = lds_bytes(prm.H);
+template <int LS, bool TERRAIN>
+static void launch_variant(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                           int batch, double* grf, int32_t* status, int32_t* iters, double* scratch,
+                           hipStream_t stream) {
+    const size_t lds = lds_bytes(prm.H, TERRAIN);
     const dim3 grid(batch), block(LMPC_WAVE);  // LMPC_SYNC() relies on exactly one wavefront per workgroup
-    if (4 * prm.H <= 64) {
-        (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(lmpc_qp_kernel<1>, grid, block, lds, stream, prm, rec, contact, batch, grf, status, iters,
-                           scratch);
+    (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<LS, TERRAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL((lmpc_qp_kernel<LS, TERRAIN>), grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
+                       status, iters, scratch);
+}
+
+// Host-side launcher (called from lmpc_capi.cpp).  normals == nullptr: flat ground (the reference).
+hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                     int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, hipStream_t stream) {
+    const bool two = 4 * prm.H > 64;
+    if (normals) {
+        if (two) launch_variant<2, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
+        else launch_variant<1, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
     } else {
-        (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(lmpc_qp_kernel<2>, grid, block, lds, stream, prm, rec, contact, batch, grf, status, iters,
-                           scratch);
+        if (two) launch_variant<2, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
+        else launch_variant<1, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
     }
     return hipGetLastError();
 }

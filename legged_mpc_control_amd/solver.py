@@ -53,24 +53,32 @@ class BatchedConvexQPSolver:
         N.check(self._L.lmpc_set_params(self._ctx, ctypes.byref(p)), "lmpc_set_params")
         self.params = p
 
-    def solve(self, rec: np.ndarray, contact: np.ndarray):
-        """Host arrays in -> (grf [B,H,12], status [B], iters [B]); synchronous."""
+    def solve(self, rec: np.ndarray, contact: np.ndarray, normals: np.ndarray | None = None):
+        """Host arrays in -> (grf [B,H,12], status [B], iters [B]); synchronous.
+        normals [B,4,3] (terrain extension) or None = flat ground (the reference problem)."""
         rec = np.ascontiguousarray(rec, dtype=np.float64)
         contact = np.ascontiguousarray(contact, dtype=np.uint8)
         B = rec.shape[0]
         if rec.shape != (B, self.record_len) or contact.shape != (B, self.H, 4):
             raise ValueError("bad record/contact shape")
+        nptr = None
+        if normals is not None:
+            normals = np.ascontiguousarray(normals, dtype=np.float64)
+            if normals.shape != (B, 4, 3):
+                raise ValueError("normals must be [B, 4, 3]")
+            nptr = _dp(normals)
         grf = np.zeros((B, self.H, 12), dtype=np.float64)
         status = np.zeros(B, dtype=np.int32)
         iters = np.zeros(B, dtype=np.int32)
-        N.check(self._L.lmpc_solve_batch(self._ctx, _dp(rec), contact.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
-                                         B, _dp(grf), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-                                         iters.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "lmpc_solve_batch")
+        N.check(self._L.lmpc_solve_batch_ex(self._ctx, _dp(rec), contact.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                            nptr, B, _dp(grf), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                            iters.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "lmpc_solve_batch_ex")
         return grf, status, iters
 
-    def solve_device(self, rec, contact, grf, status=None, iters=None, stream=None) -> None:
+    def solve_device(self, rec, contact, grf, status=None, iters=None, stream=None, normals=None) -> None:
         """Device tensors (torch, resident in HBM) in/out; asynchronous on `stream`
-        (a torch.cuda.Stream or raw hipStream_t int; default = torch's current stream)."""
+        (a torch.cuda.Stream or raw hipStream_t int; default = torch's current stream).
+        normals: optional f64 device tensor [B,4,3] (terrain extension)."""
         import torch
 
         B = rec.shape[0]
@@ -79,13 +87,16 @@ class BatchedConvexQPSolver:
                 raise ValueError("solve_device expects contiguous device tensors (f64 rec/grf, u8 contact)")
         if rec.shape != (B, self.record_len) or contact.shape != (B, self.H, 4) or grf.shape != (B, self.H, 12):
             raise ValueError("bad record/contact/grf shape")
+        if normals is not None and (not normals.is_cuda or normals.dtype != torch.float64 or
+                                    not normals.is_contiguous() or tuple(normals.shape) != (B, 4, 3)):
+            raise ValueError("normals must be a contiguous f64 device tensor [B, 4, 3]")
         if stream is None:
             stream = torch.cuda.current_stream(rec.device)
         sptr = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
-        N.check(self._L.lmpc_solve_batch_device(
-            self._ctx, rec.data_ptr(), contact.data_ptr(), B, grf.data_ptr(),
-            None if status is None else status.data_ptr(), None if iters is None else iters.data_ptr(),
-            sptr), "lmpc_solve_batch_device")
+        N.check(self._L.lmpc_solve_batch_device_ex(
+            self._ctx, rec.data_ptr(), contact.data_ptr(), None if normals is None else normals.data_ptr(), B,
+            grf.data_ptr(), None if status is None else status.data_ptr(),
+            None if iters is None else iters.data_ptr(), sptr), "lmpc_solve_batch_device_ex")
 
     def close(self) -> None:
         if self._ctx:

@@ -21,6 +21,7 @@ CONFIGS = {
     5: dict(name="go1_trot_h30_b4096", robot="go1", gait=N.GAIT_TROT, H=30, batch=4096, standing=False),
 }
 BASE_SEED = 20261015
+TERRAIN_THETA_MAX = 0.3  # config 4 terrain tilt, theta ~ U(0, 0.3) rad
 
 
 def params(robot: str = "go1") -> N.LmpcParams:
@@ -60,6 +61,31 @@ def fill(p: N.LmpcParams, cfg: N.LmpcSynthCfg, H: int, count: int, seed: int, fi
                                  con.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
     N.check(rc, "lmpc_synth_fill")
     return rec, con
+
+
+def normals(count: int, seed: int, first_index: int = 0, theta_max: float = TERRAIN_THETA_MAX) -> np.ndarray:
+    """Per-leg terrain normals [count, 4, 3] (own Philox stream; records are unaffected)."""
+    out = np.zeros((count, 4, 3), dtype=np.float64)
+    N.check(N.lib().lmpc_synth_normals(seed, first_index, count, float(theta_max),
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "lmpc_synth_normals")
+    return out
+
+
+def terrain_frame(n) -> np.ndarray:
+    """Contact frame R (columns t1, t2, n) of a ground normal (lmpc_terrain_frame)."""
+    n = np.ascontiguousarray(n, dtype=np.float64).reshape(3)
+    R = np.zeros(9)
+    N.lib().lmpc_terrain_frame(n.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                               R.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return R.reshape(3, 3)
+
+
+def config_normals(config_id: int, count: int | None = None, first_index: int = 0):
+    """Terrain normals of a config (config 4 only; None = flat ground for the others)."""
+    if config_id != 4:
+        return None
+    n = CONFIGS[config_id]["batch"] if count is None else count
+    return normals(n, BASE_SEED + config_id, first_index)
 
 
 def config_batch(config_id: int, count: int | None = None, first_index: int = 0, H: int | None = None):

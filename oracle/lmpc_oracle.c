@@ -95,9 +95,28 @@ static int in_b_pattern(int r, int c) {
     return 0;
 }
 
+/* Terrain extension: contact frame of a unit ground normal n.
+ * Columns of R (row-major) are t1, t2, n; R is the minimal rotation taking e_z
+ * to n (Rodrigues about e_z x n), so n = e_z gives R = I exactly and the
+ * rotated pyramid below is the reference's. */
+void oracle_terrain_frame(const double nin[3], double R[9]) {
+    const double nn = sqrt(nin[0] * nin[0] + nin[1] * nin[1] + nin[2] * nin[2]);
+    const double nx = nin[0] / nn, ny = nin[1] / nn, c = nin[2] / nn;
+    const double h = 1.0 / (1.0 + c);
+    R[0] = 1.0 - nx * nx * h; R[1] = -nx * ny * h;      R[2] = nx;
+    R[3] = -nx * ny * h;      R[4] = 1.0 - ny * ny * h; R[5] = ny;
+    R[6] = -nx;               R[7] = -ny;               R[8] = c;
+}
+
 void oracle_build_sparse_qp(const oracle_params* p, int H, const double* rec,
                             const uint8_t* contact, double* P_diag, double* q,
                             double* A, double* l, double* u) {
+    oracle_build_sparse_qp_ex(p, H, rec, contact, NULL, P_diag, q, A, l, u);
+}
+
+void oracle_build_sparse_qp_ex(const oracle_params* p, int H, const double* rec,
+                               const uint8_t* contact, const double* normals, double* P_diag,
+                               double* q, double* A, double* l, double* u) {
     const int n = 24 * H, m = 32 * H;
     const int dyn = 12 * H, fric = 16 * H;
     const double* x0 = rec + ORACLE_REC_X0;
@@ -121,15 +140,31 @@ void oracle_build_sparse_qp(const oracle_params* p, int H, const double* rec,
     for (int i = 0; i < H; ++i)
         for (int k = 0; k < 12; ++k) A[(size_t)(12 * i + k) * n + 24 * i + 12 + k] = -1.0;
 
-    /* friction rows (ConvexQPSolver.cpp:131-158) */
+    /* per-leg contact frames (terrain extension; flat ground = identity) */
+    double Rn[4][9];
+    for (int j = 0; j < 4; ++j) {
+        if (normals) oracle_terrain_frame(normals + 3 * j, Rn[j]);
+        else for (int e = 0; e < 9; ++e) Rn[j][e] = (e % 4 == 0) ? 1.0 : 0.0;
+    }
+    /* friction rows (ConvexQPSolver.cpp:131-158), on g = R'f: rows t1+-mu n, t2+-mu n */
     for (int i = 0; i < H; ++i)
         for (int j = 0; j < 4; ++j) {
             const int row = dyn + 16 * i + 4 * j;
             const int cx = 24 * i + 3 * j;
-            A[(size_t)(row + 0) * n + cx + 0] = 1.0; A[(size_t)(row + 0) * n + cx + 2] = p->mu;
-            A[(size_t)(row + 1) * n + cx + 0] = 1.0; A[(size_t)(row + 1) * n + cx + 2] = -p->mu;
-            A[(size_t)(row + 2) * n + cx + 1] = 1.0; A[(size_t)(row + 2) * n + cx + 2] = p->mu;
-            A[(size_t)(row + 3) * n + cx + 1] = 1.0; A[(size_t)(row + 3) * n + cx + 2] = -p->mu;
+            if (!normals) {
+                A[(size_t)(row + 0) * n + cx + 0] = 1.0; A[(size_t)(row + 0) * n + cx + 2] = p->mu;
+                A[(size_t)(row + 1) * n + cx + 0] = 1.0; A[(size_t)(row + 1) * n + cx + 2] = -p->mu;
+                A[(size_t)(row + 2) * n + cx + 1] = 1.0; A[(size_t)(row + 2) * n + cx + 2] = p->mu;
+                A[(size_t)(row + 3) * n + cx + 1] = 1.0; A[(size_t)(row + 3) * n + cx + 2] = -p->mu;
+            } else {
+                const double* R = Rn[j];
+                for (int k = 0; k < 3; ++k) {
+                    A[(size_t)(row + 0) * n + cx + k] = R[3 * k + 0] + p->mu * R[3 * k + 2];
+                    A[(size_t)(row + 1) * n + cx + k] = R[3 * k + 0] - p->mu * R[3 * k + 2];
+                    A[(size_t)(row + 2) * n + cx + k] = R[3 * k + 1] + p->mu * R[3 * k + 2];
+                    A[(size_t)(row + 3) * n + cx + k] = R[3 * k + 1] - p->mu * R[3 * k + 2];
+                }
+            }
             l[row + 0] = 0.0;          u[row + 0] = ORACLE_INF;
             l[row + 1] = -ORACLE_INF;  u[row + 1] = 0.0;
             l[row + 2] = 0.0;          u[row + 2] = ORACLE_INF;
@@ -139,7 +174,8 @@ void oracle_build_sparse_qp(const oracle_params* p, int H, const double* rec,
     for (int i = 0; i < H; ++i) {
         for (int j = 0; j < 4; ++j) {
             const int row = dyn + fric + 4 * i + j;
-            A[(size_t)row * n + 24 * i + 3 * j + 2] = 1.0;
+            if (!normals) A[(size_t)row * n + 24 * i + 3 * j + 2] = 1.0;
+            else for (int k = 0; k < 3; ++k) A[(size_t)row * n + 24 * i + 3 * j + k] = Rn[j][3 * k + 2];
             l[row] = 0.0;
             u[row] = (double)contact[4 * i + j] * p->f_max;
         }
@@ -483,6 +519,11 @@ int oracle_gi_solve(int n, const double* G, const double* g0, int m, const doubl
  * ------------------------------------------------------------------------- */
 int oracle_solve(const oracle_params* p, int H, const double* rec, const uint8_t* contact,
                  double* grf, double* kkt, int* n_active) {
+    return oracle_solve_ex(p, H, rec, contact, NULL, grf, kkt, n_active);
+}
+
+int oracle_solve_ex(const oracle_params* p, int H, const double* rec, const uint8_t* contact,
+                    const double* normals, double* grf, double* kkt, int* n_active) {
     const int n = 24 * H, m = 32 * H, N = 12 * H;
     const int dyn = 12 * H, fric = 16 * H;
     int rc = 0;
@@ -497,8 +538,8 @@ int oracle_solve(const oracle_params* p, int H, const double* rec, const uint8_t
     int* umap = (int*)malloc((size_t)N * sizeof(int));   /* U index -> free index or -1 */
     const int max_ineq = 2 * (m - dyn);
     int* cptr = (int*)malloc((size_t)(max_ineq + 1) * sizeof(int));
-    int* cidx = (int*)malloc((size_t)max_ineq * 2 * sizeof(int));
-    double* cval = (double*)malloc((size_t)max_ineq * 2 * sizeof(double));
+    int* cidx = (int*)malloc((size_t)max_ineq * 3 * sizeof(int));   /* <= 3 nonzeros per row */
+    double* cval = (double*)malloc((size_t)max_ineq * 3 * sizeof(double));
     double* c0 = (double*)malloc((size_t)max_ineq * sizeof(double));
     double *Hf = NULL, *gf = NULL, *xf = NULL, *lam = NULL;
     void* work = NULL;
@@ -506,7 +547,7 @@ int oracle_solve(const oracle_params* p, int H, const double* rec, const uint8_t
         rc = -10;
         goto out;
     }
-    oracle_build_sparse_qp(p, H, rec, contact, P, q, A, l, u);
+    oracle_build_sparse_qp_ex(p, H, rec, contact, normals, P, q, A, l, u);
     if (oracle_condense(H, P, q, A, l, Hc, g, NULL, NULL) != 0) { rc = -11; goto out; }
 
     /* swing leg-steps: bound row u == l == 0 and the friction rows force
@@ -611,6 +652,7 @@ typedef struct batch_job {
     int H, b0, b1;
     const double* rec;
     const uint8_t* contact;
+    const double* normals;
     double* grf;
     int32_t* status;
     int fails;
@@ -620,8 +662,9 @@ static void* batch_worker(void* arg) {
     batch_job* j = (batch_job*)arg;
     const int rl = 33 + 12 * j->H;
     for (int b = j->b0; b < j->b1; ++b) {
-        const int rc = oracle_solve(j->p, j->H, j->rec + (size_t)b * rl, j->contact + (size_t)b * 4 * j->H,
-                                    j->grf + (size_t)b * 12 * j->H, NULL, NULL);
+        const int rc = oracle_solve_ex(j->p, j->H, j->rec + (size_t)b * rl, j->contact + (size_t)b * 4 * j->H,
+                                       j->normals ? j->normals + (size_t)b * 12 : NULL,
+                                       j->grf + (size_t)b * 12 * j->H, NULL, NULL);
         if (j->status) j->status[b] = rc;
         if (rc != 0) j->fails++;
     }
@@ -630,13 +673,19 @@ static void* batch_worker(void* arg) {
 
 int oracle_solve_batch(const oracle_params* p, int H, int batch, const double* rec,
                        const uint8_t* contact, double* grf, int32_t* status, int n_threads) {
+    return oracle_solve_batch_ex(p, H, batch, rec, contact, NULL, grf, status, n_threads);
+}
+
+int oracle_solve_batch_ex(const oracle_params* p, int H, int batch, const double* rec,
+                          const uint8_t* contact, const double* normals, double* grf,
+                          int32_t* status, int n_threads) {
     if (n_threads < 1) n_threads = 1;
     if (n_threads > batch) n_threads = batch > 0 ? batch : 1;
     pthread_t* th = (pthread_t*)malloc((size_t)n_threads * sizeof(pthread_t));
     batch_job* jobs = (batch_job*)calloc((size_t)n_threads, sizeof(batch_job));
     int fails = 0;
     for (int t = 0; t < n_threads; ++t) {
-        jobs[t].p = p; jobs[t].H = H; jobs[t].rec = rec; jobs[t].contact = contact;
+        jobs[t].p = p; jobs[t].H = H; jobs[t].rec = rec; jobs[t].contact = contact; jobs[t].normals = normals;
         jobs[t].grf = grf; jobs[t].status = status;
         jobs[t].b0 = (int)((long long)batch * t / n_threads);
         jobs[t].b1 = (int)((long long)batch * (t + 1) / n_threads);

@@ -65,6 +65,22 @@ void oracle_build_sparse_qp(const oracle_params* p, int H, const double* rec,
                             const uint8_t* contact, double* P_diag, double* q,
                             double* A, double* l, double* u);
 
+/* Terrain extension (beyond the reference, which is
+ * flat-ground only).  normals[4][3] = per-leg ground normal (need not be unit,
+ * n_z > 0), constant over the horizon; NULL = flat ground = the reference.
+ * The reference's pyramid and f_max bound act on g = R'f, R = oracle_terrain_frame(n)
+ * (columns t1, t2, n; R = I exactly for n = e_z). */
+void oracle_terrain_frame(const double n[3], double R[9]);
+void oracle_build_sparse_qp_ex(const oracle_params* p, int H, const double* rec,
+                               const uint8_t* contact, const double* normals, double* P_diag,
+                               double* q, double* A, double* l, double* u);
+int oracle_solve_ex(const oracle_params* p, int H, const double* rec, const uint8_t* contact,
+                    const double* normals, double* grf, double* kkt, int* n_active);
+/* normals[batch][4][3] or NULL */
+int oracle_solve_batch_ex(const oracle_params* p, int H, int batch, const double* rec,
+                          const uint8_t* contact, const double* normals, double* grf,
+                          int32_t* status, int n_threads);
+
 /* Reference helper restatements (for unit tests). Row-major 12x12. */
 void oracle_update_A(double dt, double yaw, double Ad[144]);
 void oracle_update_B(const oracle_params* p, const double rot[9], const double feet[12],

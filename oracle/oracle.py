@@ -35,9 +35,10 @@ class OracleParams(ctypes.Structure):
 
 
 def build(force: bool = False) -> str:
-    """Compile the oracle with gcc (make) into oracle/build/."""
-    if force or not os.path.exists(_LIB_PATH):
-        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    """Compile the oracle with gcc (make) into oracle/build/ (make rebuilds it when the sources changed)."""
+    src = os.path.join(_HERE, "lmpc_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or (os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_LIB_PATH)):
+        subprocess.run(["make", "-s", "-C", _HERE] + (["-B"] if force else []), check=True)
     return _LIB_PATH
 
 
@@ -62,6 +63,14 @@ def lib():
             L.oracle_solve.restype = ctypes.c_int
             L.oracle_solve_batch.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, u8p, dp, i32p, ctypes.c_int]
             L.oracle_solve_batch.restype = ctypes.c_int
+            L.oracle_terrain_frame.argtypes = [dp, dp]
+            L.oracle_terrain_frame.restype = None
+            L.oracle_build_sparse_qp_ex.argtypes = [pp, ctypes.c_int, dp, u8p, dp, dp, dp, dp, dp, dp]
+            L.oracle_build_sparse_qp_ex.restype = None
+            L.oracle_solve_ex.argtypes = [pp, ctypes.c_int, dp, u8p, dp, dp, dp, ip]
+            L.oracle_solve_ex.restype = ctypes.c_int
+            L.oracle_solve_batch_ex.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, u8p, dp, dp, i32p, ctypes.c_int]
+            L.oracle_solve_batch_ex.restype = ctypes.c_int
             L.oracle_gi_solve.argtypes = [ctypes.c_int, dp, dp, ctypes.c_int, dp, dp, dp, dp, ip]
             L.oracle_gi_solve.restype = ctypes.c_int
             L.oracle_predict_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double]
@@ -101,12 +110,30 @@ def params_from(struct) -> OracleParams:
     return p
 
 
-def build_sparse_qp(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray):
+def _normals(normals, lead=()):
+    """None (flat ground, the reference) or a contiguous float64 [..., 4, 3] array."""
+    if normals is None:
+        return None, None
+    a = np.ascontiguousarray(normals, dtype=np.float64).reshape(tuple(lead) + (4, 3))
+    return a, _dp(a)
+
+
+def terrain_frame(n) -> np.ndarray:
+    """Contact frame R (columns t1, t2, n) of a ground normal; R = I for n = e_z."""
+    n = np.ascontiguousarray(n, dtype=np.float64).reshape(3)
+    R = np.zeros(9)
+    lib().oracle_terrain_frame(_dp(n), _dp(R))
+    return R.reshape(3, 3)
+
+
+def build_sparse_qp(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray, normals=None):
     n, m = 24 * H, 32 * H
     rec = np.ascontiguousarray(rec, dtype=np.float64)
     contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    nrm, nrm_p = _normals(normals)
     P = np.zeros(n); q = np.zeros(n); A = np.zeros((m, n)); l = np.zeros(m); u = np.zeros(m)
-    lib().oracle_build_sparse_qp(ctypes.byref(p), H, _dp(rec), _u8p(contact), _dp(P), _dp(q), _dp(A), _dp(l), _dp(u))
+    lib().oracle_build_sparse_qp_ex(ctypes.byref(p), H, _dp(rec), _u8p(contact), nrm_p,
+                                    _dp(P), _dp(q), _dp(A), _dp(l), _dp(u))
     return P, q, A, l, u
 
 
@@ -121,24 +148,27 @@ def condense(H: int, P, q, A, l):
     return Hc, g, T, c
 
 
-def solve(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray):
-    """Exact optimum of one instance -> (grf[H,12], kkt[4], n_active)."""
+def solve(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray, normals=None):
+    """Exact optimum of one instance -> (grf[H,12], kkt[4], n_active).  normals[4,3] or None (flat)."""
     rec = np.ascontiguousarray(rec, dtype=np.float64)
     contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    nrm, nrm_p = _normals(normals)
     grf = np.zeros(12 * H); kkt = np.zeros(4); na = ctypes.c_int(0)
-    rc = lib().oracle_solve(ctypes.byref(p), H, _dp(rec), _u8p(contact), _dp(grf), _dp(kkt), ctypes.byref(na))
+    rc = lib().oracle_solve_ex(ctypes.byref(p), H, _dp(rec), _u8p(contact), nrm_p, _dp(grf), _dp(kkt),
+                               ctypes.byref(na))
     if rc != 0:
         raise RuntimeError(f"oracle_solve failed: {rc}")
     return grf.reshape(H, 12), kkt, na.value
 
 
-def solve_batch(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray, n_threads: int = 1):
+def solve_batch(p: OracleParams, H: int, rec: np.ndarray, contact: np.ndarray, n_threads: int = 1, normals=None):
     B = rec.shape[0]
     rec = np.ascontiguousarray(rec, dtype=np.float64)
     contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    nrm, nrm_p = _normals(normals, (B,))
     grf = np.zeros((B, H, 12)); status = np.zeros(B, dtype=np.int32)
-    fails = lib().oracle_solve_batch(ctypes.byref(p), H, B, _dp(rec), _u8p(contact), _dp(grf),
-                                     status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n_threads)
+    fails = lib().oracle_solve_batch_ex(ctypes.byref(p), H, B, _dp(rec), _u8p(contact), nrm_p, _dp(grf),
+                                        status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n_threads)
     return grf, status, fails
 
 

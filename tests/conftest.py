@@ -36,7 +36,8 @@ def load_golden(path):
     pr = d["params"]
     op = O.make_params(pr[0:12], pr[12:24], pr[24], pr[25:34].reshape(3, 3), pr[34], pr[35], pr[36], pr[37])
     return dict(H=int(d["H"]), op=op, params=pr, rec=d["rec"], contact=d["contact"], grf=d["grf"],
-                kkt=d["kkt"], n_active=d["n_active"], meta=[str(m) for m in d["meta"]])
+                kkt=d["kkt"], n_active=d["n_active"], meta=[str(m) for m in d["meta"]],
+                normals=d["normals"] if "normals" in d.files else None)
 
 
 def lmpc_params_from(pr):

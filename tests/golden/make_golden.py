@@ -43,7 +43,21 @@ def skew(v):
     return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
 
 
-def ref_sparse_qp(q_w, r_w, mass, Ib, mu, fmax, g, dt, H, rec, contact):
+def rodrigues_frame(n):
+    """Terrain extension: rotation about axis e_z x n by angle acos(n_z) (Rodrigues' formula),
+    the independent restatement of lmpc_terrain_frame / oracle_terrain_frame."""
+    n = np.asarray(n, dtype=np.float64) / np.linalg.norm(n)
+    ax = np.cross([0.0, 0.0, 1.0], n)
+    s = np.linalg.norm(ax)
+    if s == 0.0:
+        return np.eye(3)
+    k = ax / s
+    K = skew(k)
+    th = np.arctan2(s, n[2])
+    return np.eye(3) + np.sin(th) * K + (1.0 - np.cos(th)) * (K @ K)
+
+
+def ref_sparse_qp(q_w, r_w, mass, Ib, mu, fmax, g, dt, H, rec, contact, normals=None):
     nx = nu = 12
     n, m = (nx + nu) * H, (nx + 16 + 4) * H
     dyn, fric = nx * H, 16 * H
@@ -85,14 +99,14 @@ def ref_sparse_qp(q_w, r_w, mass, Ib, mu, fmax, g, dt, H, rec, contact):
         for j in range(4):
             rr = dyn + 16 * i + 4 * j
             c = 24 * i + 3 * j
-            A[rr + 0, c + 0], A[rr + 0, c + 2] = 1, mu
-            A[rr + 1, c + 0], A[rr + 1, c + 2] = 1, -mu
-            A[rr + 2, c + 1], A[rr + 2, c + 2] = 1, mu
-            A[rr + 3, c + 1], A[rr + 3, c + 2] = 1, -mu
+            # pyramid rows on the contact-frame force g = Rn' f (Rn = I: the reference rows)
+            Rn = np.eye(3) if normals is None else rodrigues_frame(normals[j])
+            C = np.array([[1, 0, mu], [1, 0, -mu], [0, 1, mu], [0, 1, -mu], [0, 0, 1.0]]) @ Rn.T
+            A[rr:rr + 4, c:c + 3] = C[:4]
             l[rr:rr + 4] = [0, -INF, 0, -INF]
             u[rr:rr + 4] = [INF, 0, INF, 0]
             b = dyn + fric + 4 * i + j
-            A[b, c + 2] = 1
+            A[b, c:c + 3] = C[4]
             l[b] = 0
             u[b] = fmax * contact[i, j]
     return P, q, A, l, u
@@ -139,18 +153,20 @@ def kkt_certificate(P, q, A, l, u, grf, H):
 
 
 # ---------------------------------------------------------------------------
-def make_set(name, p, H, rec, con, meta):
+def make_set(name, p, H, rec, con, meta, normals=None):
     op = O.params_from(p)
     qw, rw = np.array(p.q_weights[:]), np.array(p.r_weights[:])
     Ib = np.array(p.trunk_inertia[:]).reshape(3, 3)
     grfs, kkts, nacts, certs = [], [], [], []
     for b in range(rec.shape[0]):
-        Po, qo, Ao, lo, uo = O.build_sparse_qp(op, H, rec[b], con[b])
-        Pn, qn, An, ln, un = ref_sparse_qp(qw, rw, p.robot_mass, Ib, p.mu, p.f_max, p.gravity, p.dt, H, rec[b], con[b])
+        nb = None if normals is None else normals[b]
+        Po, qo, Ao, lo, uo = O.build_sparse_qp(op, H, rec[b], con[b], normals=nb)
+        Pn, qn, An, ln, un = ref_sparse_qp(qw, rw, p.robot_mass, Ib, p.mu, p.f_max, p.gravity, p.dt, H, rec[b], con[b],
+                                           normals=nb)
         for a, c, what in ((Po, Pn, "P"), (qo, qn, "q"), (Ao, An, "A"), (lo, ln, "l"), (uo, un, "u")):
             err = np.max(np.abs(a - c) / np.maximum(1.0, np.abs(c)))
             assert err < 1e-13, f"{name}[{b}]: oracle assembly differs from numpy restatement in {what}: {err}"
-        grf, kkt, na = O.solve(op, H, rec[b], con[b])
+        grf, kkt, na = O.solve(op, H, rec[b], con[b], normals=nb)
         stat, viol = kkt_certificate(Pn, qn, An, ln, un, grf, H)
         assert stat < 1e-8 and viol < 1e-9, f"{name}[{b}]: KKT certificate failed stat={stat} viol={viol}"
         grfs.append(grf)
@@ -160,9 +176,10 @@ def make_set(name, p, H, rec, con, meta):
     out = os.path.join(HERE, f"golden_{name}.npz")
     params = np.concatenate([p.q_weights[:], p.r_weights[:], [p.robot_mass], p.trunk_inertia[:],
                              [p.mu, p.f_max, p.gravity, p.dt]])
+    extra = {} if normals is None else {"normals": np.asarray(normals, dtype=np.float64)}
     np.savez_compressed(out, H=np.int64(H), params=params, rec=rec, contact=con, grf=np.array(grfs),
                         kkt=np.array(kkts), n_active=np.array(nacts), certificate=np.array(certs),
-                        meta=np.array(meta))
+                        meta=np.array(meta), **extra)
     print(f"{out}: {rec.shape[0]} instances, max certificate {np.max(certs):.2e}")
 
 
@@ -212,6 +229,19 @@ def main():
         p, H, rec, con = synth.config_batch(cid, count=cnt)
         make_set(f"config{cid}_{synth.CONFIGS[cid]['name']}", p, H, rec, con,
                  [f"{synth.CONFIGS[cid]['name']} global index {i}" for i in range(cnt)])
+    # config 4 with its terrain normals (extension; parity vs this build's oracle only)
+    p4, H4, rec4, con4 = synth.config_batch(4, count=16)
+    nrm4 = synth.config_normals(4, count=16)
+    for n in nrm4.reshape(-1, 3):  # the product's frame equals the Rodrigues restatement
+        assert np.max(np.abs(synth.terrain_frame(n) - rodrigues_frame(n))) < 1e-15
+    make_set("config4t_go1_mixed_terrain_h10", p4, H4, rec4, con4,
+             [f"go1_mixed_h10_b65536 + terrain normals, global index {i}" for i in range(16)], normals=nrm4)
+    # terrain edge cases: steep tilt (theta = 0.6) so friction faces bind, and flat normals (= reference)
+    rec_e, con_e, meta_e = edge_cases(synth.params("go1"), 10)
+    nrm_e = synth.normals(rec_e.shape[0], 777, theta_max=0.6)
+    nrm_e[7] = [0.0, 0.0, 1.0]
+    meta_e = [m + " + steep terrain (theta <= 0.6)" for m in meta_e[:7]] + ["regular trot, flat normals (= reference)"]
+    make_set("edge_go1_terrain_h10", synth.params("go1"), 10, rec_e, con_e, meta_e, normals=nrm_e)
     p = synth.params("go1")
     for H in (10, 30):
         rec, con, meta = edge_cases(p, H)

@@ -46,7 +46,7 @@ def torch_dev():
 def test_golden_fixtures(path):
     g = load_golden(path)
     s = BatchedConvexQPSolver(lmpc_params_from(g["params"]), g["H"], max_batch=g["rec"].shape[0])
-    grf, status, iters = s.solve(g["rec"], g["contact"])
+    grf, status, iters = s.solve(g["rec"], g["contact"], normals=g["normals"])
     assert np.all(status == 0), status
     err = rel_err(grf, g["grf"])
     assert err <= TOL
@@ -251,3 +251,83 @@ def test_solve_options_and_status_codes():
     s.set_options(o)
     grf, status, iters = s.solve(rec, con)
     assert np.all(status == 0)
+
+
+# ---------------------------------------------------------------------------
+# terrain extension (config 4: per-leg normals, theta ~ U(0, 0.3)); parity vs this build's oracle
+# ---------------------------------------------------------------------------
+def terrain_violation(grf, con, normals, mu=0.3, fmax=180.0):
+    """Max pyramid/bound violation of g = R_j'f in each leg's contact frame."""
+    B, H = grf.shape[0], con.shape[1]
+    f = grf.reshape(B, H, 4, 3)
+    v = -np.inf
+    for j in range(4):
+        Rs = np.stack([synth.terrain_frame(n) for n in normals[:, j]])   # [B,3,3]
+        g = np.einsum("bhp,bpq->bhq", f[:, :, j], Rs)                     # g = R'f (row form)
+        c = con[:, :, j].astype(bool)
+        v = max(v, float(np.max(np.maximum.reduce([np.abs(g[..., 0]) - mu * g[..., 2],
+                                                   np.abs(g[..., 1]) - mu * g[..., 2],
+                                                   -g[..., 2], g[..., 2] - fmax * c]))))
+    return v
+
+
+def test_terrain_live_samples_vs_oracle():
+    p, H, rec, con = synth.config_batch(4, count=512, first_index=20000)
+    nrm = synth.config_normals(4, count=512, first_index=20000)
+    s = BatchedConvexQPSolver(p, H, max_batch=512)
+    grf, status, iters = s.solve(rec, con, normals=nrm)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8, normals=nrm)
+    assert fails == 0 and np.all(status == 0)
+    err = rel_err(grf, ref)
+    assert err <= TOL and err <= TOL_REGRESS, err
+    assert terrain_violation(grf, con, nrm, p.mu, p.f_max) <= 1e-9 * p.f_max
+
+
+def test_terrain_flat_normals_equal_flat_path():
+    """normals = e_z poses the reference's problem: same answer as the flat kernel (to rounding)."""
+    p, H, rec, con = synth.config_batch(4, count=256)
+    s = BatchedConvexQPSolver(p, H, max_batch=256)
+    g0, st0, _ = s.solve(rec, con)
+    g1, st1, _ = s.solve(rec, con, normals=np.tile([0.0, 0.0, 1.0], (256, 4, 1)))
+    assert np.all(st0 == 0) and np.all(st1 == 0)
+    assert rel_err(g1, g0) <= 1e-10  # same QP; G0 R is formed in a different order (rounding only)
+
+
+def test_terrain_full_size_properties(torch_dev):
+    """Config 4 at full batch (65536) with terrain: converged, feasible in every contact frame,
+    swing legs exactly zero, device path == host path, sampled against the oracle."""
+    import torch
+
+    p, H, rec, con = synth.config_batch(4)
+    nrm = synth.config_normals(4)
+    B = rec.shape[0]
+    s = BatchedConvexQPSolver(p, H, max_batch=1024)
+    d_rec, d_con = torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev)
+    d_nrm = torch.from_numpy(nrm).to(torch_dev)
+    out = torch.empty((B, H, 12), dtype=torch.float64, device=torch_dev)
+    st = torch.empty(B, dtype=torch.int32, device=torch_dev)
+    s.solve_device(d_rec, d_con, out, st, normals=d_nrm)
+    torch.cuda.synchronize()
+    grf, status = out.cpu().numpy(), st.cpu().numpy()
+    assert np.all(status == 0), np.bincount(status)
+    assert terrain_violation(grf, con, nrm, p.mu, p.f_max) <= 1e-9 * p.f_max
+    assert not np.any(grf.reshape(B, H, 4, 3)[~con.astype(bool)] != 0.0)
+    gh, sh, _ = s.solve(rec[:1024], con[:1024], normals=nrm[:1024])
+    assert np.array_equal(gh, grf[:1024]) and np.array_equal(sh, status[:1024])
+    idx = np.random.default_rng(4).choice(B, 32, replace=False)
+    ref, _, _ = O.solve_batch(O.params_from(p), H, rec[idx], con[idx], n_threads=8, normals=nrm[idx])
+    assert rel_err(grf[idx], ref) <= TOL_REGRESS
+
+
+def test_terrain_rejects_bad_normals():
+    p, H, rec, con = synth.config_batch(4, count=4)
+    s = BatchedConvexQPSolver(p, H, max_batch=4)
+    bad = np.tile([0.0, 0.0, 1.0], (4, 4, 1))
+    bad[2, 1] = [0.3, 0.0, -0.1]  # n_z <= 0: not a ground normal
+    with pytest.raises(RuntimeError):
+        s.solve(rec, con, normals=bad)
+    bad[2, 1] = [np.nan, 0.0, 1.0]
+    with pytest.raises(RuntimeError):
+        s.solve(rec, con, normals=bad)
+    with pytest.raises(ValueError):
+        s.solve(rec, con, normals=np.zeros((4, 3)))

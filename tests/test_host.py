@@ -123,3 +123,22 @@ def test_presets_match_reference_yaml():
     assert p.robot_mass == 13.0 and p.mu == 0.3 and p.f_max == 180.0 and p.gravity == 9.8 and p.dt == 0.01
     a1 = synth.params("a1")  # gazebo_a1_convex.yaml:40-72
     assert list(a1.q_weights) == [60.0, 100.0, 0.0, 0.0, 0.0, 450.0, 0.15, 0.15, 100.0, 3.0, 3.0, 5.0]
+
+
+def test_synth_normals_deterministic_and_distributed():
+    """Config 4 terrain normals: unit, tilt theta in [0, 0.3], shard-invariant, own stream."""
+    a = synth.normals(4096, 77)
+    b = synth.normals(1000, 77, first_index=3000)
+    assert np.array_equal(a[3000:4000], b)
+    assert np.allclose(np.linalg.norm(a, axis=2), 1.0, atol=1e-15)
+    th = np.arccos(np.clip(a[..., 2], -1, 1))
+    assert th.min() >= 0.0 and th.max() <= 0.3 + 1e-12
+    assert abs(th.mean() - 0.15) < 0.005  # U(0, 0.3)
+    ph = np.arctan2(a[..., 1], a[..., 0])
+    assert abs(ph.mean()) < 0.05 and ph.std() > 1.7  # U(-pi, pi): std pi/sqrt(3) = 1.81
+    # records do not depend on whether normals are drawn (separate Philox stream)
+    _, _, rec1, con1 = synth.config_batch(4, count=8)
+    synth.config_normals(4, count=8)
+    _, _, rec2, con2 = synth.config_batch(4, count=8)
+    assert np.array_equal(rec1, rec2) and np.array_equal(con1, con2)
+    assert synth.config_normals(2) is None
