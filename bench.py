@@ -36,7 +36,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall seconds)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--flat", action="store_true", help="config 4 without its terrain normals (reference problem)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     return ap.parse_args()
+
+
+def global_batch_of(strong, cfg, B, world):
+    return cfg["batch"] if strong else B * world
 
 
 def main():
@@ -100,6 +106,34 @@ def main():
     t_max = D.max_over_ranks(elapsed, dist, dev)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
+    # N > 1: a second timed pass, solve + grouped point-to-point gather of every rank's GRFs to
+    # rank 0 (SURVEY.md 8e "with and without the gather"); reported beside `value`, never as it.
+    with_gather = None
+    if dist is not None and not args.no_gather:
+        if strong:
+            counts = [b - a for a, b in (D.split_range(r, world, cfg["batch"]) for r in range(world))]
+        else:
+            counts = [B] * world
+        full = D.gather_to_rank0(d_grf, dist, world, rank, counts)  # warm the p2p channels
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            assert full.shape[0] == sum(counts) and torch.equal(full[:B], d_grf)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        for i in range(args.steps):
+            solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream, normals=d_nrm)
+            full = D.gather_to_rank0(d_grf, dist, world, rank, counts)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tg = D.max_over_ranks(time.perf_counter() - tg, dist, dev)
+        with_gather = {
+            "value": global_batch_of(strong, cfg, B, world) * args.steps / tg,
+            "ms_per_step": tg / args.steps * 1e3,
+            "gather_bytes": int(sum(counts[1:]) * H * 12 * 8),
+            "how": "solve + grouped isend/irecv of all GRFs to rank 0 (batch_isend_irecv over RCCL)",
+        }
+
     grf = d_grf.cpu().numpy()
     st = d_st.cpu().numpy()
     it = d_it.cpu().numpy()
@@ -108,7 +142,7 @@ def main():
     flop_per_qp = roofline.survey_flop(H, ipm_mean, pol_mean)  # SURVEY.md 8(d) contract figure
     riccati_flop_per_qp = roofline.qp_flop(H, ipm_mean, pol_mean)  # the build's own useful-flop count
     achieved_tf = flop_per_qp * B / (kernel_ms * 1e-3) / 1e12
-    global_batch = cfg["batch"] if strong else B * world
+    global_batch = global_batch_of(strong, cfg, B, world)
     total_qps = global_batch * args.steps / t_max
 
     stats = D.sum_over_ranks([(st == 0).sum(), (st == 1).sum(), (st == 2).sum()], dist, dev)
@@ -188,6 +222,7 @@ def main():
                 "hbm_gbs": roofline.qp_bytes(H) * B / (kernel_ms * 1e-3) / 1e9,
             },
             "cpu_baseline": cpu,
+            "with_gather": with_gather,
             "max_grf_err": max_err,
             "qp_status": {"converged": int(stats[0]), "max_iter": int(stats[1]), "nan": int(stats[2])},
             "ipm_iters_mean": ipm_mean,

@@ -49,19 +49,26 @@ def sum_over_ranks(values, dist, device=None):
     return [float(v) for v in t.tolist()]
 
 
-def gather_to_rank0(tensor, dist, world: int, rank: int):
-    """Gather equally-shaped per-rank result tensors to rank 0 with point-to-point
-    sends (ordered by rank).  Returns the concatenation on rank 0, None elsewhere."""
+def gather_to_rank0(tensor, dist, world: int, rank: int, counts=None):
+    """Gather per-rank result tensors (leading dim = that rank's QP count) to rank 0.
+
+    One grouped point-to-point exchange (batch_isend_irecv = ncclGroupStart / ncclSend x
+    (N-1) / ncclRecv x (N-1) / ncclGroupEnd on RCCL): every sender uses its own direct xGMI
+    link to rank 0, nothing is relayed around a ring.  `counts[r]` = rows
+    owned by rank r (default: all equal).  Returns the concatenation on rank 0, None elsewhere.
+    """
     import torch
 
     if dist is None or world == 1:
         return tensor
+    if counts is None:
+        counts = [tensor.shape[0]] * world
     if rank == 0:
-        parts = [tensor]
-        for src in range(1, world):
-            buf = torch.empty_like(tensor)
-            dist.recv(buf, src=src)
-            parts.append(buf)
-        return torch.cat(parts, dim=0)
-    dist.send(tensor, dst=0)
-    return None
+        bufs = [tensor] + [torch.empty((counts[src],) + tuple(tensor.shape[1:]), dtype=tensor.dtype,
+                                       device=tensor.device) for src in range(1, world)]
+        ops = [dist.P2POp(dist.irecv, bufs[src], src) for src in range(1, world)]
+    else:
+        ops = [dist.P2POp(dist.isend, tensor, 0)]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    return torch.cat(bufs, dim=0) if rank == 0 else None
