@@ -184,6 +184,32 @@ typedef struct lmpc_state_in {
 int lmpc_pack_record(const lmpc_params* p, int horizon, const lmpc_state_in* st, double* rec,
                      double lin_vel_d_world[3]);
 
+/* ---- the step before the QP, on the device --------------
+ * One command per instance = what calc_mpc_reference and update_bound_constraints
+ * read (ConvexQPSolver.cpp:254-313,329-346) plus the contact FSM state
+ * (LeggedContactFSM.cpp:280-294).  The device expands commands into records and
+ * contact schedules in HBM: 384 B in per instance instead of 33+12H doubles and
+ * 4H bytes, and no host preprocessing.  The expansion is bit-identical to
+ * lmpc_pack_record + lmpc_contact_schedule on the host. */
+typedef struct lmpc_command {
+    lmpc_state_in state;
+    double gait_phase;        /* FSM phase in [0, 1) */
+    double gait_speed;        /* phase per second */
+    int32_t gait;             /* LMPC_GAIT_* */
+    uint8_t plan_contacts[4]; /* step-0 contacts (ctrl.plan_contacts) */
+} lmpc_command;
+
+/* host: one command -> rec[33+12H], contact[H][4] */
+int lmpc_command_to_record(const lmpc_params* p, int horizon, const lmpc_command* cmd, double* rec,
+                           uint8_t* contact);
+/* device: d_cmd[batch] -> d_rec[batch][33+12H], d_contact[batch][H][4] (async on stream) */
+int lmpc_build_records_device(lmpc_ctx* ctx, const lmpc_command* d_cmd, int batch, double* d_rec,
+                              uint8_t* d_contact, void* stream);
+/* device: expand into the context's own buffers, then solve (one call per control tick) */
+int lmpc_solve_commands_device(lmpc_ctx* ctx, const lmpc_command* d_cmd, const double* d_normals,
+                               int batch, double* d_grf, int32_t* d_status, int32_t* d_iters,
+                               void* stream);
+
 /* ---- synthetic batches, counter-based (Philox4x32-10) ---- */
 typedef struct lmpc_synth_cfg {
     int gait;             /* LMPC_GAIT_*, or -1 = mixed (uniform over the four) */
@@ -202,6 +228,16 @@ int lmpc_synth_fill(const lmpc_params* p, const lmpc_synth_cfg* cfg, int horizon
  * from lmpc_synth_fill's, so records are identical with and without normals. */
 int lmpc_synth_normals(uint64_t seed, int64_t first_index, int count, double theta_max,
                        double* normals /* [count][4][3] */);
+/* Synthetic commands (lmpc_synth_fill == lmpc_synth_commands + lmpc_command_to_record).  The
+ * device variants generate the same instances from (seed, global index) in HBM, so no input
+ * bytes cross PCIe or xGMI; they agree with the host generator to a few ulp
+ * (the device math library's sin/cos/log). */
+int lmpc_synth_commands(const lmpc_synth_cfg* cfg, uint64_t seed, int64_t first_index, int count,
+                        lmpc_command* cmd);
+int lmpc_synth_commands_device(lmpc_ctx* ctx, const lmpc_synth_cfg* cfg, uint64_t seed,
+                               int64_t first_index, int count, lmpc_command* d_cmd, void* stream);
+int lmpc_synth_normals_device(lmpc_ctx* ctx, uint64_t seed, int64_t first_index, int count,
+                              double theta_max, double* d_normals, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,9 @@ EXPORTED_SYMBOLS = (
     "lmpc_synth_cfg_go1", "lmpc_synth_cfg_a1_standing", "lmpc_synth_fill",
     # ABI 2: terrain extension
     "lmpc_terrain_frame", "lmpc_solve_batch_ex", "lmpc_solve_batch_device_ex", "lmpc_synth_normals",
+    # on-device input generation
+    "lmpc_command_to_record", "lmpc_build_records_device", "lmpc_solve_commands_device",
+    "lmpc_synth_commands", "lmpc_synth_commands_device", "lmpc_synth_normals_device",
 )
 ABI_VERSION = 2
 
@@ -78,6 +81,19 @@ class LmpcSynthCfg(ctypes.Structure):
         ("default_feet", ctypes.c_double * 12),
         ("standing", ctypes.c_int),
     ]
+
+
+class LmpcCommand(ctypes.Structure):
+    _fields_ = [
+        ("state", LmpcStateIn),
+        ("gait_phase", ctypes.c_double),
+        ("gait_speed", ctypes.c_double),
+        ("gait", ctypes.c_int32),
+        ("plan_contacts", ctypes.c_uint8 * 4),
+    ]
+
+
+COMMAND_BYTES = ctypes.sizeof(LmpcCommand)  # 384
 
 
 class NativeLibraryError(RuntimeError):
@@ -147,6 +163,20 @@ def lib():
         L.lmpc_solve_batch_device_ex.restype = ctypes.c_int
         L.lmpc_synth_normals.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_double, dp]
         L.lmpc_synth_normals.restype = ctypes.c_int
+        cp = ctypes.POINTER(LmpcCommand)
+        L.lmpc_command_to_record.argtypes = [pp, ctypes.c_int, cp, dp, u8p]
+        L.lmpc_command_to_record.restype = ctypes.c_int
+        L.lmpc_build_records_device.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp]
+        L.lmpc_build_records_device.restype = ctypes.c_int
+        L.lmpc_solve_commands_device.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
+        L.lmpc_solve_commands_device.restype = ctypes.c_int
+        L.lmpc_synth_commands.argtypes = [ctypes.POINTER(LmpcSynthCfg), ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, cp]
+        L.lmpc_synth_commands.restype = ctypes.c_int
+        L.lmpc_synth_commands_device.argtypes = [vp, ctypes.POINTER(LmpcSynthCfg), ctypes.c_uint64, ctypes.c_int64,
+                                                 ctypes.c_int, vp, vp]
+        L.lmpc_synth_commands_device.restype = ctypes.c_int
+        L.lmpc_synth_normals_device.argtypes = [vp, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp]
+        L.lmpc_synth_normals_device.restype = ctypes.c_int
         if L.lmpc_abi_version() != ABI_VERSION:
             raise NativeLibraryError("liblmpc.so ABI version mismatch")
         _lib = L

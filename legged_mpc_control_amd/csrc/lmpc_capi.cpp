@@ -16,6 +16,12 @@
 namespace lmpc {
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                      int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, hipStream_t stream);
+hipError_t launch_records(const lmpc_command* cmd, int batch, int H, double dt, double* rec, uint8_t* contact,
+                          hipStream_t stream);
+hipError_t launch_synth(const lmpc_synth_cfg& cfg, uint64_t seed, int64_t first, int count, lmpc_command* cmd,
+                        hipStream_t stream);
+hipError_t launch_normals(uint64_t seed, int64_t first, int count, double theta_max, double* normals,
+                          hipStream_t stream);
 }
 
 struct lmpc_ctx {
@@ -32,6 +38,9 @@ struct lmpc_ctx {
     int32_t* d_iters = nullptr;
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
     size_t scratch_qps = 0;
+    double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
+    uint8_t* d_ccon = nullptr;
+    size_t cmd_qps = 0;
 };
 
 namespace {
@@ -76,6 +85,11 @@ void free_bufs(lmpc_ctx* c) {
     (void)hipFree(c->d_scratch);
     c->d_scratch = nullptr;
     c->scratch_qps = 0;
+    (void)hipFree(c->d_crec);
+    (void)hipFree(c->d_ccon);
+    c->d_crec = nullptr;
+    c->d_ccon = nullptr;
+    c->cmd_qps = 0;
     c->d_rec = nullptr;
     c->d_contact = nullptr;
     c->d_normals = nullptr;
@@ -232,6 +246,59 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
 int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int batch, double* grf,
                      int32_t* status, int32_t* iters) {
     return lmpc_solve_batch_ex(c, rec, contact, nullptr, batch, grf, status, iters);
+}
+
+static int launch_rc(hipError_t e) {
+    if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
+    return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
+}
+
+int lmpc_build_records_device(lmpc_ctx* c, const lmpc_command* d_cmd, int batch, double* d_rec, uint8_t* d_contact,
+                              void* stream) {
+    if (!c || batch < 0 || (batch > 0 && (!d_cmd || !d_rec || !d_contact))) return LMPC_ERR_ARG;
+    if (batch == 0) return LMPC_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch_rc(lmpc::launch_records(d_cmd, batch, c->H, c->prm.dt, d_rec, d_contact, s));
+}
+
+int lmpc_solve_commands_device(lmpc_ctx* c, const lmpc_command* d_cmd, const double* d_normals, int batch,
+                               double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
+    if (!c || batch < 0 || (batch > 0 && (!d_cmd || !d_grf))) return LMPC_ERR_ARG;
+    if (batch == 0) return LMPC_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if ((size_t)batch > c->cmd_qps) {
+        if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
+        (void)hipDeviceSynchronize();  // the old buffers may still be read by queued work
+        (void)hipFree(c->d_crec);
+        (void)hipFree(c->d_ccon);
+        c->d_crec = nullptr;
+        c->d_ccon = nullptr;
+        c->cmd_qps = 0;
+        if (hipMalloc(&c->d_crec, (size_t)batch * lmpc_record_len(c->H) * sizeof(double)) != hipSuccess ||
+            hipMalloc(&c->d_ccon, (size_t)batch * 4 * c->H) != hipSuccess)
+            return LMPC_ERR_ALLOC;
+        c->cmd_qps = (size_t)batch;
+    }
+    int rc = lmpc_build_records_device(c, d_cmd, batch, c->d_crec, c->d_ccon, s);
+    if (rc != LMPC_OK) return rc;
+    return lmpc_solve_batch_device_ex(c, c->d_crec, c->d_ccon, d_normals, batch, d_grf, d_status, d_iters, s);
+}
+
+int lmpc_synth_commands_device(lmpc_ctx* c, const lmpc_synth_cfg* cfg, uint64_t seed, int64_t first_index, int count,
+                               lmpc_command* d_cmd, void* stream) {
+    if (!c || !cfg || count < 0 || (count > 0 && !d_cmd)) return LMPC_ERR_ARG;
+    if (count == 0) return LMPC_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch_rc(lmpc::launch_synth(*cfg, seed, first_index, count, d_cmd, s));
+}
+
+int lmpc_synth_normals_device(lmpc_ctx* c, uint64_t seed, int64_t first_index, int count, double theta_max,
+                              double* d_normals, void* stream) {
+    if (!c || count < 0 || (count > 0 && !d_normals) || !(theta_max >= 0.0) || theta_max >= 1.5707963267948966)
+        return LMPC_ERR_ARG;
+    if (count == 0) return LMPC_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch_rc(lmpc::launch_normals(seed, first_index, count, theta_max, d_normals, s));
 }
 
 int lmpc_sync(lmpc_ctx* c) {

@@ -13,101 +13,8 @@
 #include <cstring>
 
 #include "lmpc/lmpc.h"
+#include "lmpc_common.h"
 
-namespace {
-
-struct GaitTab {
-    int size;
-    int state[3];
-    double sw[3];
-};
-
-GaitTab gait_table(int gait, int leg) {
-    GaitTab t{};
-    switch (gait) {
-    case LMPC_GAIT_CRAWL:  // LeggedContactFSM.cpp:158-199
-        if (leg == 0) t = {2, {0, 1, 0}, {0.25, 1.0, 0.0}};
-        else if (leg == 1) t = {3, {1, 0, 1}, {0.25, 0.5, 1.0}};
-        else if (leg == 2) t = {3, {1, 0, 1}, {0.5, 0.75, 1.0}};
-        else t = {2, {1, 0, 0}, {0.75, 1.0, 0.0}};
-        break;
-    case LMPC_GAIT_TROT_WITH_STAND:  // LeggedContactFSM.cpp:116-156
-        if (leg == 0 || leg == 3) t = {2, {1, 0, 0}, {0.6, 1.0, 0.0}};
-        else t = {3, {1, 0, 1}, {0.1, 0.5, 1.0}};
-        break;
-    case LMPC_GAIT_STAND:  // LeggedContactFSM.cpp:201-212
-        t = {1, {1, 0, 0}, {1.0, 0.0, 0.0}};
-        break;
-    default:  // trot, LeggedContactFSM.cpp:93-114
-        if (leg == 0 || leg == 3) t = {2, {1, 0, 0}, {0.5, 1.0, 0.0}};
-        else t = {2, {0, 1, 0}, {0.5, 1.0, 0.0}};
-        break;
-    }
-    return t;
-}
-
-// ---- Philox4x32-10 counter-based generator --------------------------------
-struct Philox {
-    uint32_t key[2];
-    uint32_t ctr[4];
-    uint32_t out[4];
-    int used;
-
-    Philox(uint64_t seed, uint64_t index, uint32_t stream = 0x4c4d5043u /* "LMPC" */) {
-        key[0] = (uint32_t)seed;
-        key[1] = (uint32_t)(seed >> 32);
-        ctr[0] = (uint32_t)index;
-        ctr[1] = (uint32_t)(index >> 32);
-        ctr[2] = 0;
-        ctr[3] = stream;
-        used = 4;
-    }
-    void block() {
-        uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
-        uint32_t k0 = key[0], k1 = key[1];
-        for (int r = 0; r < 10; ++r) {
-            const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-            const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-            const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-            const uint32_t n1 = (uint32_t)p1;
-            const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-            const uint32_t n3 = (uint32_t)p0;
-            c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
-            k0 += 0x9E3779B9u;
-            k1 += 0xBB67AE85u;
-        }
-        for (int i = 0; i < 4; ++i) out[i] = c[i];
-        ctr[2]++;
-        used = 0;
-    }
-    uint32_t next32() {
-        if (used >= 4) block();
-        return out[used++];
-    }
-    // uniform in [0,1) with 53 random bits
-    double uniform() {
-        const uint32_t a = next32() >> 5, b = next32() >> 6;
-        return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
-    }
-    double uniform(double lo, double hi) { return lo + (hi - lo) * uniform(); }
-    double normal(double sigma) {
-        const double u1 = 1.0 - uniform();  // (0,1]
-        const double u2 = uniform();
-        return sigma * std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
-    }
-};
-
-void euler_zyx_to_rot(double roll, double pitch, double yaw, double R[9]) {
-    const double cr = std::cos(roll), sr = std::sin(roll);
-    const double cp = std::cos(pitch), sp = std::sin(pitch);
-    const double cy = std::cos(yaw), sy = std::sin(yaw);
-    // R = Rz(yaw) * Ry(pitch) * Rx(roll)
-    R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
-    R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
-    R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
-}
-
-}  // namespace
 
 extern "C" {
 
@@ -159,19 +66,11 @@ const char* lmpc_strerror(int code) {
 }
 
 int lmpc_predict_contact(int gait, int leg, double gait_phase, double gait_speed, double dt) {
-    const GaitTab t = gait_table(gait, leg);
-    double ph = gait_phase + gait_speed * dt;
-    while (ph > 1.0) ph -= 1.0;
-    for (int i = 0; i < t.size; ++i)
-        if (ph <= t.sw[i]) return t.state[i];
-    return 1;  // "should not reach here" -> STANCE
+    return lmpc_common::predict_contact(gait, leg, gait_phase, gait_speed, dt);
 }
 
 int lmpc_current_contact(int gait, int leg, double gait_phase) {
-    const GaitTab t = gait_table(gait, leg);
-    for (int i = 0; i < t.size; ++i)
-        if (gait_phase < t.sw[i]) return t.state[i];
-    return t.state[t.size - 1];
+    return lmpc_common::current_contact(gait, leg, gait_phase);
 }
 
 int lmpc_contact_schedule(int gait, double gait_phase, double gait_speed, double dt, int horizon,
@@ -243,58 +142,28 @@ void lmpc_synth_cfg_a1_standing(lmpc_synth_cfg* c) {
     c->standing = 1;
 }
 
+int lmpc_command_to_record(const lmpc_params* p, int horizon, const lmpc_command* cmd, double* rec,
+                           uint8_t* contact) {
+    if (!p || !cmd || !rec || !contact || horizon < 1) return LMPC_ERR_ARG;
+    lmpc_pack_record(p, horizon, &cmd->state, rec, nullptr);
+    return lmpc_contact_schedule(cmd->gait, cmd->gait_phase, cmd->gait_speed, p->dt, horizon, cmd->plan_contacts,
+                                 contact);
+}
+
+int lmpc_synth_commands(const lmpc_synth_cfg* cfg, uint64_t seed, int64_t first_index, int count, lmpc_command* cmd) {
+    if (!cfg || !cmd || count < 0) return LMPC_ERR_ARG;
+    for (int b = 0; b < count; ++b) lmpc_common::synth_command(*cfg, seed, (uint64_t)(first_index + b), cmd[b]);
+    return LMPC_OK;
+}
+
 int lmpc_synth_fill(const lmpc_params* p, const lmpc_synth_cfg* cfg, int horizon, uint64_t seed,
                     int64_t first_index, int count, double* rec, uint8_t* contact) {
     if (!p || !cfg || !rec || !contact || horizon < 1 || count < 0) return LMPC_ERR_ARG;
     const int rl = lmpc_record_len(horizon);
     for (int b = 0; b < count; ++b) {
-        lmpc_state_in st;
-        std::memset(&st, 0, sizeof(st));
-        double phase = 0.0;
-        int gait = cfg->gait < 0 ? LMPC_GAIT_TROT : cfg->gait;
-        uint8_t plan[4] = {1, 1, 1, 1};
-        if (cfg->standing) {
-            // config 1: x0=[0,0,0, 0,0,0.30, 0..], z_d = 0.30, v_d = 0, all plan_contacts = 1,
-            // FSM reset (phase 0): ConvexMpc.cpp:86-92 standing mode.
-            st.root_pos[2] = 0.30;
-            st.root_pos_d[2] = 0.30;
-            euler_zyx_to_rot(0.0, 0.0, 0.0, st.root_rot_mat);
-            for (int j = 0; j < 12; ++j) st.foot_pos_abs[j] = cfg->default_feet[j];
-        } else {
-            Philox rng(seed, (uint64_t)(first_index + b));
-            const double roll = rng.uniform(-0.2, 0.2);
-            const double pitch = rng.uniform(-0.2, 0.2);
-            const double yaw = rng.uniform(-M_PI, M_PI);
-            st.root_euler[0] = roll;
-            st.root_euler[1] = pitch;
-            st.root_euler[2] = yaw;
-            st.root_pos[0] = rng.uniform(-1.0, 1.0);
-            st.root_pos[1] = rng.uniform(-1.0, 1.0);
-            st.root_pos[2] = rng.uniform(0.20, 0.35);
-            for (int k = 0; k < 3; ++k) st.root_ang_vel[k] = rng.normal(0.3);
-            st.root_lin_vel[0] = rng.uniform(-1.0, 1.0);
-            st.root_lin_vel[1] = rng.uniform(-1.0, 1.0);
-            st.root_lin_vel[2] = rng.normal(0.1);
-            st.root_pos_d[2] = rng.uniform(0.25, 0.32);
-            st.root_lin_vel_d_rel[0] = rng.uniform(-1.0, 1.0);
-            st.root_lin_vel_d_rel[1] = rng.uniform(-0.4, 0.4);
-            st.root_ang_vel_d_rel[2] = rng.uniform(-0.8, 0.8);
-            euler_zyx_to_rot(roll, pitch, yaw, st.root_rot_mat);
-            const double* R = st.root_rot_mat;
-            for (int j = 0; j < 4; ++j) {
-                double rel[3];
-                for (int k = 0; k < 3; ++k) rel[k] = cfg->default_feet[3 * j + k] + rng.uniform(-0.03, 0.03);
-                for (int r = 0; r < 3; ++r)
-                    st.foot_pos_abs[3 * j + r] = R[3 * r] * rel[0] + R[3 * r + 1] * rel[1] + R[3 * r + 2] * rel[2];
-            }
-            phase = rng.uniform();
-            if (cfg->gait < 0) gait = (int)(rng.uniform() * 4.0) & 3;
-            for (int j = 0; j < 4; ++j) plan[j] = (uint8_t)lmpc_current_contact(gait, j, phase);
-        }
-        double* r = rec + (size_t)b * rl;
-        lmpc_pack_record(p, horizon, &st, r, nullptr);
-        lmpc_contact_schedule(gait, phase, cfg->gait_speed, p->dt, horizon, plan,
-                              contact + (size_t)b * 4 * horizon);
+        lmpc_command c;
+        lmpc_common::synth_command(*cfg, seed, (uint64_t)(first_index + b), c);
+        lmpc_command_to_record(p, horizon, &c, rec + (size_t)b * rl, contact + (size_t)b * 4 * horizon);
     }
     return LMPC_OK;
 }
@@ -311,17 +180,8 @@ void lmpc_terrain_frame(const double nin[3], double R[9]) {
 
 int lmpc_synth_normals(uint64_t seed, int64_t first_index, int count, double theta_max, double* normals) {
     if (!normals || count < 0 || !(theta_max >= 0.0) || theta_max >= 1.5707963267948966) return LMPC_ERR_ARG;
-    for (int b = 0; b < count; ++b) {
-        Philox rng(seed, (uint64_t)(first_index + b), 0x54455252u /* "TERR" */);
-        for (int j = 0; j < 4; ++j) {
-            const double th = rng.uniform(0.0, theta_max);
-            const double ph = rng.uniform(-M_PI, M_PI);
-            double* n = normals + (size_t)b * 12 + 3 * j;
-            n[0] = std::sin(th) * std::cos(ph);
-            n[1] = std::sin(th) * std::sin(ph);
-            n[2] = std::cos(th);
-        }
-    }
+    for (int b = 0; b < count; ++b)
+        lmpc_common::synth_normals(seed, (uint64_t)(first_index + b), theta_max, normals + (size_t)b * 12);
     return LMPC_OK;
 }
 

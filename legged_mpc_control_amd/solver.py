@@ -98,6 +98,66 @@ class BatchedConvexQPSolver:
             grf.data_ptr(), None if status is None else status.data_ptr(),
             None if iters is None else iters.data_ptr(), sptr), "lmpc_solve_batch_device_ex")
 
+    # ---- the step before the QP, on the device -------------------------------
+    # Commands live in HBM as an opaque uint8 tensor [B, N.COMMAND_BYTES] (lmpc_command array).
+    @staticmethod
+    def _stream(stream, dev):
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+    def synth_commands_device(self, cfg: N.LmpcSynthCfg, count: int, seed: int, first_index: int = 0, device=None,
+                              stream=None):
+        """Synthetic commands generated on the device from (seed, global index) -> uint8 [count, 384]."""
+        import torch
+
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+        out = torch.empty((count, N.COMMAND_BYTES), dtype=torch.uint8, device=dev)
+        N.check(self._L.lmpc_synth_commands_device(self._ctx, ctypes.byref(cfg), seed, first_index, count,
+                                                   out.data_ptr(), self._stream(stream, dev)),
+                "lmpc_synth_commands_device")
+        return out
+
+    def synth_normals_device(self, count: int, seed: int, first_index: int = 0, theta_max: float = 0.3, device=None,
+                             stream=None):
+        import torch
+
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+        out = torch.empty((count, 4, 3), dtype=torch.float64, device=dev)
+        N.check(self._L.lmpc_synth_normals_device(self._ctx, seed, first_index, count, float(theta_max),
+                                                  out.data_ptr(), self._stream(stream, dev)),
+                "lmpc_synth_normals_device")
+        return out
+
+    def build_records_device(self, cmd, stream=None):
+        """uint8 [B, 384] commands in HBM -> (rec [B, 33+12H] f64, contact [B, H, 4] u8) in HBM."""
+        import torch
+
+        B = cmd.shape[0]
+        if not cmd.is_cuda or cmd.dtype != torch.uint8 or tuple(cmd.shape) != (B, N.COMMAND_BYTES):
+            raise ValueError("commands must be a uint8 device tensor [B, COMMAND_BYTES]")
+        rec = torch.empty((B, self.record_len), dtype=torch.float64, device=cmd.device)
+        con = torch.empty((B, self.H, 4), dtype=torch.uint8, device=cmd.device)
+        N.check(self._L.lmpc_build_records_device(self._ctx, cmd.data_ptr(), B, rec.data_ptr(), con.data_ptr(),
+                                                  self._stream(stream, cmd.device)), "lmpc_build_records_device")
+        return rec, con
+
+    def solve_commands_device(self, cmd, grf, status=None, iters=None, stream=None, normals=None) -> None:
+        """commands -> records (context buffers) -> solve, all on `stream`."""
+        import torch
+
+        B = cmd.shape[0]
+        if not cmd.is_cuda or cmd.dtype != torch.uint8 or tuple(cmd.shape) != (B, N.COMMAND_BYTES):
+            raise ValueError("commands must be a uint8 device tensor [B, COMMAND_BYTES]")
+        if grf.shape != (B, self.H, 12) or grf.dtype != torch.float64 or not grf.is_cuda:
+            raise ValueError("bad grf tensor")
+        N.check(self._L.lmpc_solve_commands_device(
+            self._ctx, cmd.data_ptr(), None if normals is None else normals.data_ptr(), B, grf.data_ptr(),
+            None if status is None else status.data_ptr(), None if iters is None else iters.data_ptr(),
+            self._stream(stream, cmd.device)), "lmpc_solve_commands_device")
+
     def close(self) -> None:
         if self._ctx:
             self._L.lmpc_destroy(self._ctx)

@@ -88,6 +88,28 @@ def config_normals(config_id: int, count: int | None = None, first_index: int = 
     return normals(n, BASE_SEED + config_id, first_index)
 
 
+def commands(cfg: N.LmpcSynthCfg, count: int, seed: int, first_index: int = 0):
+    """Host synthetic commands -> ctypes array of LmpcCommand (lmpc_synth_commands)."""
+    arr = (N.LmpcCommand * count)()
+    N.check(N.lib().lmpc_synth_commands(ctypes.byref(cfg), seed, first_index, count, arr), "lmpc_synth_commands")
+    return arr
+
+
+def command_to_record(p: N.LmpcParams, H: int, cmd: N.LmpcCommand):
+    """Host expansion of one command -> (rec [33+12H], contact [H, 4])."""
+    rec = np.zeros(33 + 12 * H, dtype=np.float64)
+    con = np.zeros((H, 4), dtype=np.uint8)
+    N.check(N.lib().lmpc_command_to_record(ctypes.byref(p), H, ctypes.byref(cmd),
+                                           rec.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                           con.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "lmpc_command_to_record")
+    return rec, con
+
+
+def config_cfg(config_id: int) -> N.LmpcSynthCfg:
+    c = CONFIGS[config_id]
+    return synth_cfg(c["robot"], c["gait"], c["standing"])
+
+
 def config_batch(config_id: int, count: int | None = None, first_index: int = 0, H: int | None = None):
     """Synthetic batch for a BASELINE.json config -> (params, H, rec, contact)."""
     c = CONFIGS[config_id]

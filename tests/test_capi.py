@@ -48,6 +48,8 @@ def test_struct_layouts():
     assert ctypes.sizeof(N.LmpcParams) == 8 * (12 + 12 + 1 + 9 + 4)
     assert ctypes.sizeof(N.LmpcOptions) == 4 * 3 + 4 + 8 * 3  # 3 ints + pad + 3 doubles
     assert ctypes.sizeof(N.LmpcStateIn) == 8 * (3 * 4 + 9 + 12 + 3 * 4)
+    assert ctypes.sizeof(N.LmpcCommand) == N.COMMAND_BYTES == 384  # static_assert'ed in lmpc_common.h
+    assert N.LmpcCommand.gait.offset == 376 and N.LmpcCommand.plan_contacts.offset == 380
 
 
 def test_create_rejects_bad_arguments():

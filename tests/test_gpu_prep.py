@@ -1,0 +1,93 @@
+"""GPU tests of the step before the QP on the device: command -> record
+expansion (bit-identical to the host restatement), on-device synthetic generation (== the host
+generator to a few ulp), and the fused commands -> solve path against the CPU oracle."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import rel_err
+
+from legged_mpc_control_amd import BatchedConvexQPSolver, _native as N, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def _host_cmds_tensor(cmds, dev):
+    import torch
+
+    raw = np.frombuffer(bytes(cmds), dtype=np.uint8).reshape(len(cmds), N.COMMAND_BYTES)
+    return torch.from_numpy(raw.copy()).to(dev)
+
+
+@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5])
+def test_device_expansion_bit_identical(cid, dev):
+    import torch
+
+    count = 1 if cid == 1 else 300
+    p, H, rec, con = synth.config_batch(cid, count=count, first_index=7)
+    cmds = synth.commands(synth.config_cfg(cid), count, synth.BASE_SEED + cid, first_index=7)
+    s = BatchedConvexQPSolver(p, H, max_batch=0)
+    d_rec, d_con = s.build_records_device(_host_cmds_tensor(cmds, dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(d_rec.cpu().numpy(), rec)
+    assert np.array_equal(d_con.cpu().numpy(), con)
+
+
+def test_device_generator_matches_host(dev):
+    import torch
+
+    p, H = synth.params("go1"), 10
+    cfg = synth.config_cfg(4)
+    s = BatchedConvexQPSolver(p, H, max_batch=0)
+    d_cmd = s.synth_commands_device(cfg, 4096, 123, first_index=1000, device=dev)
+    torch.cuda.synchronize()
+    host = synth.commands(cfg, 4096, 123, first_index=1000)
+    hraw = np.frombuffer(bytes(host), dtype=np.uint8).reshape(4096, N.COMMAND_BYTES)
+    draw = d_cmd.cpu().numpy()
+    hd, dd = hraw[:, :376].view(np.float64), draw[:, :376].view(np.float64)  # 45 state doubles + phase + speed
+    assert np.max(np.abs(hd - dd) / np.maximum(1.0, np.abs(hd))) <= 1e-14
+    assert np.array_equal(hraw[:, 376:], draw[:, 376:])  # gait, plan_contacts (and padding-free tail)
+    assert np.array_equal(hd[:, 45], dd[:, 45])  # gait phase: no transcendental on its path
+    # normals
+    dn = s.synth_normals_device(4096, 123, first_index=1000, device=dev)
+    torch.cuda.synchronize()
+    hn = synth.normals(4096, 123, first_index=1000)
+    assert np.max(np.abs(dn.cpu().numpy() - hn)) <= 1e-15
+
+
+@pytest.mark.parametrize("cid", [2, 4])
+def test_commands_to_solve_on_device_vs_oracle(cid, dev):
+    """Inputs generated on the device from (seed, global index), expanded and solved there; the
+    records read back feed the CPU oracle."""
+    import torch
+
+    p, H = synth.config_batch(cid, count=1)[:2]
+    B = 512
+    s = BatchedConvexQPSolver(p, H, max_batch=0)
+    d_cmd = s.synth_commands_device(synth.config_cfg(cid), B, synth.BASE_SEED + cid, first_index=40000, device=dev)
+    d_nrm = s.synth_normals_device(B, synth.BASE_SEED + cid, first_index=40000, device=dev) if cid == 4 else None
+    grf = torch.empty((B, H, 12), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    s.solve_commands_device(d_cmd, grf, st, normals=d_nrm)
+    d_rec, d_con = s.build_records_device(d_cmd)
+    torch.cuda.synchronize()
+    rec, con = d_rec.cpu().numpy(), d_con.cpu().numpy()
+    nrm = None if d_nrm is None else d_nrm.cpu().numpy()
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8, normals=nrm)
+    assert fails == 0 and np.all(st.cpu().numpy() == 0)
+    assert rel_err(grf.cpu().numpy(), ref) <= 1e-7
+    # the fused call equals expand + solve
+    grf2 = torch.empty_like(grf)
+    s.solve_device(d_rec, d_con, grf2, normals=d_nrm)
+    torch.cuda.synchronize()
+    assert torch.equal(grf, grf2)

@@ -142,3 +142,16 @@ def test_synth_normals_deterministic_and_distributed():
     _, _, rec2, con2 = synth.config_batch(4, count=8)
     assert np.array_equal(rec1, rec2) and np.array_equal(con1, con2)
     assert synth.config_normals(2) is None
+
+
+@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5])
+def test_commands_expand_to_the_generator_records(cid):
+    """lmpc_synth_fill == lmpc_synth_commands + lmpc_command_to_record, bit for bit (SURVEY.md 8f-1:
+    the command is all the step before the QP needs)."""
+    p, H, rec, con = synth.config_batch(cid, count=24, first_index=100)
+    cmds = synth.commands(synth.config_cfg(cid), 24, synth.BASE_SEED + cid, first_index=100)
+    for b in range(24):
+        r, c = synth.command_to_record(p, H, cmds[b])
+        assert np.array_equal(r, rec[b]) and np.array_equal(c, con[b])
+    if cid == 4:
+        assert len({cmds[b].gait for b in range(24)}) > 1  # mixed gaits
