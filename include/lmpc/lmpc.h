@@ -210,6 +210,28 @@ int lmpc_solve_commands_device(lmpc_ctx* ctx, const lmpc_command* d_cmd, const d
                                int batch, double* d_grf, int32_t* d_status, int32_t* d_iters,
                                void* stream);
 
+/* ---- the step after the QP: GRF -> joint torque --------
+ * BaseInterface::tau_ctrl_update (BaseInterface.cpp:451-459): per leg i,
+ *   f_rel = R' u0_i (world -> body),  tau_i = -J_i' f_rel,
+ * J_i = A1Kinematics::jac(q_i, rho_opt_i, rho_fix_i) (A1Kinematics.cpp:14-18): the body-frame
+ * foot Jacobian of the hip-abduction / hip / knee chain.  rho_fix = [leg_offset_x, leg_offset_y,
+ * motor_offset, upper_leg_length, lower_leg_length], rho_opt = foot offset (BaseInterface.cpp:76-97). */
+typedef struct lmpc_leg_kin {
+    double rho_fix[4][5];
+    double rho_opt[4][3];
+} lmpc_leg_kin;
+/* the reference's constants (BaseInterface.cpp:76-97, LeggedParams.h:24), FL FR RL RR */
+void lmpc_leg_kin_default(lmpc_leg_kin* k);
+/* J row-major: J[3*r + c] = d p_r / d q_c */
+void lmpc_foot_jacobian(const lmpc_leg_kin* k, int leg, const double q[3], double J[9]);
+/* one instance, host: rot[9] row-major, joint_pos[12], grf0[12] (u_0, world) -> tau[12] */
+int lmpc_grf_to_torque(const lmpc_leg_kin* k, const double rot[9], const double joint_pos[12],
+                       const double grf0[12], double tau[12]);
+/* batch, device: R from d_rec[b] (LMPC_REC_ROT), u_0 = d_grf[b][0][:], d_joint_pos[b][12] -> d_tau[b][12] */
+int lmpc_grf_to_torque_device(lmpc_ctx* ctx, const lmpc_leg_kin* k, const double* d_rec,
+                              const double* d_joint_pos, const double* d_grf, int batch, double* d_tau,
+                              void* stream);
+
 /* ---- synthetic batches, counter-based (Philox4x32-10) ---- */
 typedef struct lmpc_synth_cfg {
     int gait;             /* LMPC_GAIT_*, or -1 = mixed (uniform over the four) */

@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     # on-device input generation
     "lmpc_command_to_record", "lmpc_build_records_device", "lmpc_solve_commands_device",
     "lmpc_synth_commands", "lmpc_synth_commands_device", "lmpc_synth_normals_device",
+    # GRF -> joint torque
+    "lmpc_leg_kin_default", "lmpc_foot_jacobian", "lmpc_grf_to_torque", "lmpc_grf_to_torque_device",
 )
 ABI_VERSION = 2
 
@@ -94,6 +96,13 @@ class LmpcCommand(ctypes.Structure):
 
 
 COMMAND_BYTES = ctypes.sizeof(LmpcCommand)  # 384
+
+
+class LmpcLegKin(ctypes.Structure):
+    _fields_ = [
+        ("rho_fix", (ctypes.c_double * 5) * 4),
+        ("rho_opt", (ctypes.c_double * 3) * 4),
+    ]
 
 
 class NativeLibraryError(RuntimeError):
@@ -177,6 +186,15 @@ def lib():
         L.lmpc_synth_commands_device.restype = ctypes.c_int
         L.lmpc_synth_normals_device.argtypes = [vp, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp]
         L.lmpc_synth_normals_device.restype = ctypes.c_int
+        kp = ctypes.POINTER(LmpcLegKin)
+        L.lmpc_leg_kin_default.argtypes = [kp]
+        L.lmpc_leg_kin_default.restype = None
+        L.lmpc_foot_jacobian.argtypes = [kp, ctypes.c_int, dp, dp]
+        L.lmpc_foot_jacobian.restype = None
+        L.lmpc_grf_to_torque.argtypes = [kp, dp, dp, dp, dp]
+        L.lmpc_grf_to_torque.restype = ctypes.c_int
+        L.lmpc_grf_to_torque_device.argtypes = [vp, kp, vp, vp, vp, ctypes.c_int, vp, vp]
+        L.lmpc_grf_to_torque_device.restype = ctypes.c_int
         if L.lmpc_abi_version() != ABI_VERSION:
             raise NativeLibraryError("liblmpc.so ABI version mismatch")
         _lib = L

@@ -22,6 +22,8 @@ hipError_t launch_synth(const lmpc_synth_cfg& cfg, uint64_t seed, int64_t first,
                         hipStream_t stream);
 hipError_t launch_normals(uint64_t seed, int64_t first, int count, double theta_max, double* normals,
                           hipStream_t stream);
+hipError_t launch_torque(const lmpc_leg_kin& kin, const double* rec, const double* joint_pos, const double* grf,
+                         int batch, int H, double* tau, hipStream_t stream);
 }
 
 struct lmpc_ctx {
@@ -299,6 +301,14 @@ int lmpc_synth_normals_device(lmpc_ctx* c, uint64_t seed, int64_t first_index, i
     if (count == 0) return LMPC_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return launch_rc(lmpc::launch_normals(seed, first_index, count, theta_max, d_normals, s));
+}
+
+int lmpc_grf_to_torque_device(lmpc_ctx* c, const lmpc_leg_kin* k, const double* d_rec, const double* d_joint_pos,
+                              const double* d_grf, int batch, double* d_tau, void* stream) {
+    if (!c || !k || batch < 0 || (batch > 0 && (!d_rec || !d_joint_pos || !d_grf || !d_tau))) return LMPC_ERR_ARG;
+    if (batch == 0) return LMPC_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch_rc(lmpc::launch_torque(*k, d_rec, d_joint_pos, d_grf, batch, c->H, d_tau, s));
 }
 
 int lmpc_sync(lmpc_ctx* c) {

@@ -256,4 +256,35 @@ LMPC_HD inline void synth_normals(uint64_t seed, uint64_t index, double theta_ma
     }
 }
 
+// ---- GRF -> joint torque (BaseInterface.cpp:451-459) ---------------------
+// Foot position of the abduction/hip/knee chain in the body frame, for rho = (rho_fix, rho_opt):
+//   h(q1,q2) = L1 cos q1 + b cos(q1+q2) + a sin(q1+q2)   (leg extension in the sagittal plane)
+//   p = [ox - L1 sin q1 - b sin(q1+q2) + a cos(q1+q2),  oy + d cos q0 + h sin q0,  d sin q0 - h cos q0]
+// with a = rho_opt[0], b = L2 - rho_opt[2], d = motor_offset + rho_opt[1] -- the model
+// A1Kinematics::fk (A1Kinematics.cpp:8-12,38-72) evaluates.  J = dp/dq in closed form:
+LMPC_HD inline void foot_jacobian(const double rf[5], const double ro[3], const double q[3], double J[9]) {
+    LMPC_NO_FMA
+    const double L1 = rf[3], a = ro[0], b = rf[4] - ro[2], d = rf[2] + ro[1];
+    const double s0 = sin(q[0]), c0 = cos(q[0]);
+    const double s1 = sin(q[1]), c1 = cos(q[1]);
+    const double s12 = sin(q[1] + q[2]), c12 = cos(q[1] + q[2]);
+    const double h2 = b * c12 + a * s12;   // knee part of h
+    const double g2 = a * c12 - b * s12;   // d h2 / d q2
+    const double h = L1 * c1 + h2;
+    const double g = g2 - L1 * s1;         // d h / d q1
+    J[0] = 0.0;                 J[1] = -h;       J[2] = -h2;
+    J[3] = c0 * h - d * s0;     J[4] = s0 * g;   J[5] = s0 * g2;
+    J[6] = d * c0 + s0 * h;     J[7] = -c0 * g;  J[8] = -c0 * g2;
+}
+
+// tau_leg = -J' (R' f_world) for one leg (rot row-major)
+LMPC_HD inline void leg_torque(const double rf[5], const double ro[3], const double rot[9], const double q[3],
+                               const double f[3], double tau[3]) {
+    LMPC_NO_FMA
+    double fr[3], J[9];
+    for (int r = 0; r < 3; ++r) fr[r] = rot[r] * f[0] + rot[3 + r] * f[1] + rot[6 + r] * f[2];
+    foot_jacobian(rf, ro, q, J);
+    for (int c = 0; c < 3; ++c) tau[c] = -(J[c] * fr[0] + J[3 + c] * fr[1] + J[6 + c] * fr[2]);
+}
+
 }  // namespace lmpc_common

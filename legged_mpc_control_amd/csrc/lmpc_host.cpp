@@ -178,6 +178,33 @@ void lmpc_terrain_frame(const double nin[3], double R[9]) {
     R[6] = -nx;               R[7] = -ny;               R[8] = c;
 }
 
+void lmpc_leg_kin_default(lmpc_leg_kin* k) {
+    // BaseInterface.cpp:76-97 (and LOWER_LEG_LENGTH, LeggedParams.h:24); legs FL FR RL RR
+    static const double ox[4] = {0.1805, 0.1805, -0.1805, -0.1805};
+    static const double oy[4] = {0.047, -0.047, 0.047, -0.047};
+    static const double mo[4] = {0.0838, -0.0838, 0.0838, -0.0838};
+    for (int i = 0; i < 4; ++i) {
+        k->rho_fix[i][0] = ox[i];
+        k->rho_fix[i][1] = oy[i];
+        k->rho_fix[i][2] = mo[i];
+        k->rho_fix[i][3] = 0.21;
+        k->rho_fix[i][4] = 0.21;
+        k->rho_opt[i][0] = k->rho_opt[i][1] = k->rho_opt[i][2] = 0.0;
+    }
+}
+
+void lmpc_foot_jacobian(const lmpc_leg_kin* k, int leg, const double q[3], double J[9]) {
+    lmpc_common::foot_jacobian(k->rho_fix[leg & 3], k->rho_opt[leg & 3], q, J);
+}
+
+int lmpc_grf_to_torque(const lmpc_leg_kin* k, const double rot[9], const double joint_pos[12], const double grf0[12],
+                       double tau[12]) {
+    if (!k || !rot || !joint_pos || !grf0 || !tau) return LMPC_ERR_ARG;
+    for (int i = 0; i < 4; ++i)
+        lmpc_common::leg_torque(k->rho_fix[i], k->rho_opt[i], rot, joint_pos + 3 * i, grf0 + 3 * i, tau + 3 * i);
+    return LMPC_OK;
+}
+
 int lmpc_synth_normals(uint64_t seed, int64_t first_index, int count, double theta_max, double* normals) {
     if (!normals || count < 0 || !(theta_max >= 0.0) || theta_max >= 1.5707963267948966) return LMPC_ERR_ARG;
     for (int b = 0; b < count; ++b)

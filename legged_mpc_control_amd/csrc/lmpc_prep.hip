@@ -5,6 +5,7 @@
 //                         :329-346, predict_contact_state LeggedContactFSM.cpp:280-294)
 //   lmpc_synth_kernel     synthetic commands from (seed, global index)
 //   lmpc_normals_kernel   synthetic terrain normals (config 4)
+//   lmpc_torque_kernel    the step after the QP: GRF -> joint torque (BaseInterface.cpp:451-459, 8f-2)
 //
 // All three are HBM-write-bound element maps: one thread per output element (records) or per
 // instance (generators), grid-stride, consecutive threads -> consecutive addresses.  The
@@ -51,6 +52,35 @@ __global__ void __launch_bounds__(256) lmpc_normals_kernel(uint64_t seed, int64_
     lmpc_common::synth_normals(seed, (uint64_t)(first + b), theta_max, n);
 #pragma unroll
     for (int k = 0; k < 12; ++k) normals[(size_t)b * 12 + k] = n[k];
+}
+
+// one thread per (instance, leg): tau = -J'(R'u0), BaseInterface.cpp:451-459
+__global__ void __launch_bounds__(256) lmpc_torque_kernel(lmpc_leg_kin kin, const double* __restrict__ rec,
+                                                          const double* __restrict__ joint_pos,
+                                                          const double* __restrict__ grf, int batch, int H,
+                                                          double* __restrict__ tau) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 4 * batch) return;
+    const int b = t >> 2, leg = t & 3;
+    const double* R = rec + (size_t)b * (LMPC_REC_XREF + 12 * H) + LMPC_REC_ROT;
+    double rot[9], q[3], f[3], out[3];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) rot[e] = R[e];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        q[c] = joint_pos[(size_t)b * 12 + 3 * leg + c];
+        f[c] = grf[(size_t)b * 12 * H + 3 * leg + c];  // u_0
+    }
+    lmpc_common::leg_torque(kin.rho_fix[leg], kin.rho_opt[leg], rot, q, f, out);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tau[(size_t)b * 12 + 3 * leg + c] = out[c];
+}
+
+hipError_t launch_torque(const lmpc_leg_kin& kin, const double* rec, const double* joint_pos, const double* grf,
+                         int batch, int H, double* tau, hipStream_t stream) {
+    hipLaunchKernelGGL(lmpc_torque_kernel, dim3((4 * batch + 255) / 256), dim3(256), 0, stream, kin, rec, joint_pos,
+                       grf, batch, H, tau);
+    return hipGetLastError();
 }
 
 hipError_t launch_records(const lmpc_command* cmd, int batch, int H, double dt, double* rec, uint8_t* contact,

@@ -25,6 +25,30 @@ def _dp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
+def leg_kin_default() -> N.LmpcLegKin:
+    """The reference's leg constants (BaseInterface.cpp:76-97)."""
+    k = N.LmpcLegKin()
+    N.lib().lmpc_leg_kin_default(ctypes.byref(k))
+    return k
+
+
+def foot_jacobian(kin: N.LmpcLegKin, leg: int, q) -> np.ndarray:
+    q = np.ascontiguousarray(q, dtype=np.float64).reshape(3)
+    J = np.zeros(9)
+    N.lib().lmpc_foot_jacobian(ctypes.byref(kin), int(leg), _dp(q), _dp(J))
+    return J.reshape(3, 3)
+
+
+def grf_to_torque(kin: N.LmpcLegKin, rot, joint_pos, grf0) -> np.ndarray:
+    """Host: one instance, tau [12] = -J_i'(R'u0_i) (BaseInterface::tau_ctrl_update, BaseInterface.cpp:451-459)."""
+    rot = np.ascontiguousarray(rot, dtype=np.float64).reshape(9)
+    q = np.ascontiguousarray(joint_pos, dtype=np.float64).reshape(12)
+    f = np.ascontiguousarray(grf0, dtype=np.float64).reshape(12)
+    tau = np.zeros(12)
+    N.check(N.lib().lmpc_grf_to_torque(ctypes.byref(kin), _dp(rot), _dp(q), _dp(f), _dp(tau)), "lmpc_grf_to_torque")
+    return tau
+
+
 class BatchedConvexQPSolver:
     """A device context: horizon H, host staging for up to max_batch QPs."""
 
@@ -157,6 +181,23 @@ class BatchedConvexQPSolver:
             self._ctx, cmd.data_ptr(), None if normals is None else normals.data_ptr(), B, grf.data_ptr(),
             None if status is None else status.data_ptr(), None if iters is None else iters.data_ptr(),
             self._stream(stream, cmd.device)), "lmpc_solve_commands_device")
+
+    # ---- the step after the QP: GRF -> joint torque ------------------------------
+    def grf_to_torque_device(self, kin: N.LmpcLegKin, rec, joint_pos, grf, stream=None):
+        """tau [B, 12] = -J'(R'u0) per leg, from rec (R), joint_pos [B, 12] and grf [B, H, 12] in HBM."""
+        import torch
+
+        B = rec.shape[0]
+        for t in (rec, joint_pos, grf):
+            if not t.is_cuda or t.dtype != torch.float64 or not t.is_contiguous():
+                raise ValueError("grf_to_torque_device expects contiguous f64 device tensors")
+        if joint_pos.shape != (B, 12) or grf.shape != (B, self.H, 12) or rec.shape != (B, self.record_len):
+            raise ValueError("bad rec/joint_pos/grf shape")
+        tau = torch.empty((B, 12), dtype=torch.float64, device=rec.device)
+        N.check(self._L.lmpc_grf_to_torque_device(self._ctx, ctypes.byref(kin), rec.data_ptr(), joint_pos.data_ptr(),
+                                                  grf.data_ptr(), B, tau.data_ptr(), self._stream(stream, rec.device)),
+                "lmpc_grf_to_torque_device")
+        return tau
 
     def close(self) -> None:
         if self._ctx:

@@ -9,6 +9,7 @@
 #define _GNU_SOURCE
 #include "lmpc_oracle.h"
 
+#include <complex.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
@@ -751,4 +752,50 @@ int oracle_current_contact(int gait, int leg, double gait_phase) {
     for (int i = 0; i < t.size; ++i)
         if (gait_phase < t.sw[i]) return t.state[i];
     return t.state[t.size - 1];
+}
+
+/* ---------------------------------------------------------------------------
+ * GRF -> joint torque (BaseInterface.cpp:451-459)
+ * ------------------------------------------------------------------------- */
+/* A1Kinematics::fk (A1Kinematics.cpp:38-72): foot position in the body frame, written out term by
+ * term as the reference's expanded expression, for complex joint angles (complex-step derivative). */
+static void fk_complex(const double complex q[3], const double ro[3], const double rf[5], double complex p[3]) {
+    const double complex c0 = ccos(q[0]), c1 = ccos(q[1]), c2 = ccos(q[2]);
+    const double complex s0 = csin(q[0]), s1 = csin(q[1]), s2 = csin(q[2]);
+    const double complex s12 = csin(q[1] + q[2]), c12 = ccos(q[1] + q[2]);
+    p[0] = rf[0] + ro[2] * s12 - rf[4] * s12 - s1 * rf[3] + ro[0] * c12;
+    p[1] = rf[1] + ro[1] * c0 + rf[2] * c0 + c1 * s0 * rf[3] + ro[0] * c1 * s0 * s2 + ro[0] * c2 * s0 * s1
+           - ro[2] * c1 * c2 * s0 + ro[2] * s0 * s1 * s2 + rf[4] * c1 * c2 * s0 - rf[4] * s0 * s1 * s2;
+    p[2] = ro[1] * s0 + rf[2] * s0 - c0 * c1 * rf[3] - ro[0] * c0 * c1 * s2 - ro[0] * c0 * c2 * s1
+           + ro[2] * c0 * c1 * c2 - ro[2] * c0 * s1 * s2 - rf[4] * c0 * c1 * c2 + rf[4] * c0 * s1 * s2;
+}
+
+void oracle_foot_position(const double rho_fix[5], const double rho_opt[3], const double q[3], double p[3]) {
+    double complex qc[3] = {q[0], q[1], q[2]}, pc[3];
+    fk_complex(qc, rho_opt, rho_fix, pc);
+    for (int r = 0; r < 3; ++r) p[r] = creal(pc[r]);
+}
+
+/* J[3r+c] = dp_r/dq_c by complex-step differentiation (exact to rounding; no subtraction) */
+void oracle_foot_jacobian(const double rho_fix[5], const double rho_opt[3], const double q[3], double J[9]) {
+    const double h = 1e-30;
+    for (int c = 0; c < 3; ++c) {
+        double complex qc[3] = {q[0], q[1], q[2]}, pc[3];
+        qc[c] += h * I;
+        fk_complex(qc, rho_opt, rho_fix, pc);
+        for (int r = 0; r < 3; ++r) J[3 * r + c] = cimag(pc[r]) / h;
+    }
+}
+
+/* tau_i = -J_i' (R' u0_i) per leg (BaseInterface.cpp:453-458); rho_fix[4][5], rho_opt[4][3] */
+void oracle_grf_to_torque(const double* rho_fix, const double* rho_opt, const double rot[9],
+                          const double joint_pos[12], const double grf0[12], double tau[12]) {
+    for (int i = 0; i < 4; ++i) {
+        double J[9], fr[3];
+        oracle_foot_jacobian(rho_fix + 5 * i, rho_opt + 3 * i, joint_pos + 3 * i, J);
+        for (int r = 0; r < 3; ++r)
+            fr[r] = rot[r] * grf0[3 * i] + rot[3 + r] * grf0[3 * i + 1] + rot[6 + r] * grf0[3 * i + 2];
+        for (int c = 0; c < 3; ++c)
+            tau[3 * i + c] = -(J[c] * fr[0] + J[3 + c] * fr[1] + J[6 + c] * fr[2]);
+    }
 }

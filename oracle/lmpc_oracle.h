@@ -81,6 +81,15 @@ int oracle_solve_batch_ex(const oracle_params* p, int H, int batch, const double
                           const uint8_t* contact, const double* normals, double* grf,
                           int32_t* status, int n_threads);
 
+/* GRF -> joint torque, the step after the QP (BaseInterface.cpp:451-459; A1Kinematics.cpp:8-72).
+ * Foot position restated from the reference's expanded fk expression; its Jacobian by
+ * complex-step differentiation (independent of the product's closed-form Jacobian). */
+void oracle_foot_position(const double rho_fix[5], const double rho_opt[3], const double q[3], double p[3]);
+void oracle_foot_jacobian(const double rho_fix[5], const double rho_opt[3], const double q[3], double J[9]);
+void oracle_grf_to_torque(const double* rho_fix /*[4][5]*/, const double* rho_opt /*[4][3]*/,
+                          const double rot[9], const double joint_pos[12], const double grf0[12],
+                          double tau[12]);
+
 /* Reference helper restatements (for unit tests). Row-major 12x12. */
 void oracle_update_A(double dt, double yaw, double Ad[144]);
 void oracle_update_B(const oracle_params* p, const double rot[9], const double feet[12],

@@ -71,6 +71,12 @@ def lib():
             L.oracle_solve_ex.restype = ctypes.c_int
             L.oracle_solve_batch_ex.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, u8p, dp, dp, i32p, ctypes.c_int]
             L.oracle_solve_batch_ex.restype = ctypes.c_int
+            L.oracle_foot_position.argtypes = [dp, dp, dp, dp]
+            L.oracle_foot_position.restype = None
+            L.oracle_foot_jacobian.argtypes = [dp, dp, dp, dp]
+            L.oracle_foot_jacobian.restype = None
+            L.oracle_grf_to_torque.argtypes = [dp, dp, dp, dp, dp, dp]
+            L.oracle_grf_to_torque.restype = None
             L.oracle_gi_solve.argtypes = [ctypes.c_int, dp, dp, ctypes.c_int, dp, dp, dp, dp, ip]
             L.oracle_gi_solve.restype = ctypes.c_int
             L.oracle_predict_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double]
@@ -190,3 +196,29 @@ def predict_contact(gait: int, leg: int, phase: float, speed: float, dt: float) 
 
 def current_contact(gait: int, leg: int, phase: float) -> int:
     return lib().oracle_current_contact(gait, leg, phase)
+
+
+def _f64(a, n=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a if n is None else a.reshape(n)
+
+
+def foot_position(rho_fix, rho_opt, q) -> np.ndarray:
+    p = np.zeros(3)
+    lib().oracle_foot_position(_dp(_f64(rho_fix, 5)), _dp(_f64(rho_opt, 3)), _dp(_f64(q, 3)), _dp(p))
+    return p
+
+
+def foot_jacobian(rho_fix, rho_opt, q) -> np.ndarray:
+    J = np.zeros(9)
+    lib().oracle_foot_jacobian(_dp(_f64(rho_fix, 5)), _dp(_f64(rho_opt, 3)), _dp(_f64(q, 3)), _dp(J))
+    return J.reshape(3, 3)
+
+
+def grf_to_torque(rho_fix, rho_opt, rot, joint_pos, grf0) -> np.ndarray:
+    """rho_fix [4,5], rho_opt [4,3], rot [3,3] row-major, joint_pos [12], grf0 [12] -> tau [12]."""
+    tau = np.zeros(12)
+    rf, ro = _f64(rho_fix, 20), _f64(rho_opt, 12)
+    lib().oracle_grf_to_torque(_dp(rf), _dp(ro), _dp(_f64(rot, 9)), _dp(_f64(joint_pos, 12)), _dp(_f64(grf0, 12)),
+                               _dp(tau))
+    return tau

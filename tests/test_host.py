@@ -155,3 +155,43 @@ def test_commands_expand_to_the_generator_records(cid):
         assert np.array_equal(r, rec[b]) and np.array_equal(c, con[b])
     if cid == 4:
         assert len({cmds[b].gait for b in range(24)}) > 1  # mixed gaits
+
+
+def test_foot_jacobian_matches_complex_step_oracle():
+    """Closed-form J (product) == complex-step derivative of the restated A1Kinematics::fk (oracle),
+    for the reference's constants and for nonzero rho_opt."""
+    from legged_mpc_control_amd import foot_jacobian, leg_kin_default
+
+    kin = leg_kin_default()
+    assert [list(kin.rho_fix[i]) for i in range(4)] == [
+        [0.1805, 0.047, 0.0838, 0.21, 0.21], [0.1805, -0.047, -0.0838, 0.21, 0.21],
+        [-0.1805, 0.047, 0.0838, 0.21, 0.21], [-0.1805, -0.047, -0.0838, 0.21, 0.21]]  # BaseInterface.cpp:76-97
+    rng = np.random.default_rng(5)
+    for trial in range(400):
+        leg = trial % 4
+        if trial >= 200:
+            for k in range(3):
+                kin.rho_opt[leg][k] = rng.uniform(-0.03, 0.03)
+        q = rng.uniform([-0.8, -1.0, -2.7], [0.8, 2.5, -0.5])
+        J = foot_jacobian(kin, leg, q)
+        Jo = O.foot_jacobian(list(kin.rho_fix[leg]), list(kin.rho_opt[leg]), q)
+        assert np.max(np.abs(J - Jo)) <= 1e-15 * 4
+
+
+def test_grf_to_torque_matches_oracle():
+    from legged_mpc_control_amd import grf_to_torque, leg_kin_default
+
+    kin = leg_kin_default()
+    p, H, rec, con = synth.config_batch(2, count=64)
+    g = load_golden([q for q in golden_files() if "config2" in q][0])
+    rng = np.random.default_rng(9)
+    rf = np.array([list(kin.rho_fix[i]) for i in range(4)])
+    ro = np.array([list(kin.rho_opt[i]) for i in range(4)])
+    for b in range(16):
+        q = rng.uniform(np.tile([-0.3, 0.4, -2.4], 4), np.tile([0.3, 1.2, -1.2], 4))
+        tau = grf_to_torque(kin, g["rec"][b, 12:21], q, g["grf"][b, 0])
+        ref = O.grf_to_torque(rf, ro, g["rec"][b, 12:21], q, g["grf"][b, 0])
+        assert np.max(np.abs(tau - ref) / np.maximum(1.0, np.abs(ref))) <= 1e-13
+    # swing legs carry no force -> zero torque; standing (R = I, straight legs): tau = -J' f
+    tau0 = grf_to_torque(kin, np.eye(3), np.zeros(12), np.zeros(12))
+    assert np.array_equal(tau0, np.zeros(12))
