@@ -212,7 +212,7 @@ def main():
                 "global_batch": global_batch,
                 "robot": cfg["robot"],
                 "gait": "mixed" if cfg["gait"] < 0 else ["trot", "crawl", "trot_with_stand", "stand"][cfg["gait"]],
-                "terrain": None if nrm is None else f"per-leg normals, tilt U(0, {synth.TERRAIN_THETA_MAX}) rad",
+                "terrain": f"per-leg normals, tilt U(0, {synth.TERRAIN_THETA_MAX}) rad" if terrain else None,
                 "parallelism": f"dp{world} (independent QP shards, no collective)",
             },
             "roofline": {

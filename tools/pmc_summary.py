@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Turn the output of tools/profile_round.sh (gpurun_out/prof) into the committed evidence:
+profiles/<tag>/{c2,c4}_kernel_stats.csv, pmc_per_dispatch.json, pmc_calibration.json, and
+profiles/pmc_traffic.json (bytes per launch for bench.py's roofline.traffic).
+
+Calibration (tools/ubench/pmc_cal.hip, 512 MiB past the Infinity Cache): for 8-byte-per-lane
+coalesced accesses, the access width lmpc_qp_kernel uses, FETCH_SIZE reports half the bytes read
+and WRITE_SIZE reports the bytes written exactly.  The read factor is applied to FETCH_SIZE."""
+import csv
+import json
+import os
+import shutil
+import statistics as st
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "gpurun_out", "prof")
+TAG = sys.argv[1] if len(sys.argv) > 1 else "r01_final"
+DST = os.path.join(ROOT, "profiles", TAG)
+
+
+def rows(name):
+    return list(csv.DictReader(open(os.path.join(SRC, name, f"{name}_counter_collection.csv"))))
+
+
+def per_kernel(name, kern="lmpc_qp_kernel"):
+    r = [x for x in rows(name) if kern in x["Kernel_Name"]]
+    return [float(x["Counter_Value"]) for x in r], [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in r]
+
+
+def main():
+    os.makedirs(DST, exist_ok=True)
+    cal = {}
+    for tag, ctr in (("calf", "FETCH_SIZE"), ("calw", "WRITE_SIZE")):
+        for x in rows(tag):
+            cal[f"{x['Kernel_Name'].split('(')[0]}:{ctr}_KiB"] = float(x["Counter_Value"])
+    truth_kib = 512 * 1024
+    read_factor = truth_kib / cal["read8:FETCH_SIZE_KiB"]
+    write_factor = truth_kib / cal["write8:WRITE_SIZE_KiB"]
+    cal.update(read_factor=read_factor, write_factor=write_factor, bytes_moved=truth_kib * 1024,
+               note="8 B/lane coalesced; FETCH_SIZE x read_factor and WRITE_SIZE x write_factor = bytes")
+    json.dump(cal, open(os.path.join(DST, "pmc_calibration.json"), "w"), indent=1)
+
+    per = {}
+    traffic = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    for c, wl, qps in (("2", "go1_trot_h10_b1024", 1024), ("4", "go1_mixed_h10_b65536+terrain", 65536)):
+        f, fd = per_kernel(f"f{c}")
+        w, wd = per_kernel(f"w{c}")
+        fb, wb = st.mean(f) * 1024 * read_factor, st.mean(w) * 1024 * write_factor
+        per[wl] = dict(fetch_kib_raw=f, write_kib_raw=w, fetch_bytes=fb, write_bytes=wb,
+                       dispatch_ns_fetch_pass=fd, dispatch_ns_write_pass=wd)
+        traffic[wl] = {
+            "bytes_per_launch": fb + wb,
+            "bytes_per_qp": (fb + wb) / qps,
+            "fetch_bytes": fb,
+            "write_bytes": wb,
+            "source": f"profiles/{TAG}/pmc_per_dispatch.json",
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py "
+                      f"(config {c}, --no-cpu); per-dispatch mean of lmpc_qp_kernel; FETCH_SIZE x {read_factor:.3f}, "
+                      f"WRITE_SIZE x {write_factor:.3f} from profiles/{TAG}/pmc_calibration.json",
+        }
+    json.dump(per, open(os.path.join(DST, "pmc_per_dispatch.json"), "w"), indent=1)
+    json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    for c in ("c2", "c4"):
+        shutil.copy(os.path.join(SRC, c, f"{c}_kernel_stats.csv"), os.path.join(DST, f"{c}_kernel_stats.csv"))
+        shutil.copy(os.path.join(SRC, f"{c}_bench.log"), os.path.join(DST, f"{c}_bench.log"))
+    for k, v in traffic.items():
+        print(k, round(v["bytes_per_launch"] / 1e6, 1), "MB/launch")
+
+
+if __name__ == "__main__":
+    main()
