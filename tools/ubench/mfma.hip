@@ -8,6 +8,8 @@ __global__ void __launch_bounds__(64) k(double* out, unsigned long long* cyc) {
     const int lane = threadIdx.x;
     double a = 1.0 + lane * 1e-3, b = 1.0 - lane * 1e-4;
     d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+    double x[8];
+    for (int q = 0; q < 8; ++q) x[q] = lane + q;
     const unsigned long long t0 = __builtin_readcyclecounter();
 #pragma unroll 1
     for (int it = 0; it < 128; ++it) {
@@ -22,6 +24,24 @@ __global__ void __launch_bounds__(64) k(double* out, unsigned long long* cyc) {
                 c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
                 c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
             }
+        } else if (MODE == 3) {  // dependent chain + 8 independent VALU fma per MFMA (does VALU overlap?)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[q] = fma(x[q], 1.0000001, 1e-9);
+            }
+        } else if (MODE == 4) {  // only the VALU part of MODE 3 (reference)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[q] = fma(x[q], 1.0000001, 1e-9);
+        } else if (MODE == 5) {  // 2 independent accumulators
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+            }
         } else {  // result used as the next B operand (accumulator -> operand dependency)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -32,7 +52,9 @@ __global__ void __launch_bounds__(64) k(double* out, unsigned long long* cyc) {
     }
     const unsigned long long t1 = __builtin_readcyclecounter();
     d4 s = c0 + c1 + c2 + c3;
-    out[lane] = s[0] + s[1] + s[2] + s[3] + b;
+    double xs = 0.0;
+    for (int q = 0; q < 8; ++q) xs += x[q];
+    out[lane] = s[0] + s[1] + s[2] + s[3] + b + xs;
     if (lane == 0) cyc[0] = t1 - t0;
 }
 
@@ -53,12 +75,16 @@ int main() {
     (void)hipMalloc(&out, 4096 * sizeof(double));
     (void)hipMalloc(&cyc, 8 * sizeof(unsigned long long));
     unsigned long long h;
-    const char* nm[] = {"mfma f64 16x16x4 dependent acc", "mfma f64 16x16x4 4 independent", "mfma f64 acc->operand chain"};
-    for (int m = 0; m < 3; ++m) {
+    const char* nm[] = {"mfma f64 16x16x4 dependent acc", "mfma f64 16x16x4 4 independent", "mfma f64 acc->operand chain",
+                        "dep mfma + 8 indep VALU fma each", "the 8 VALU fma alone (per MFMA slot)", "mfma 2 independent"};
+    for (int m = 0; m < 6; ++m) {
         for (int rep = 0; rep < 2; ++rep) {
             if (m == 0) k<0><<<1, 64>>>(out, cyc);
             if (m == 1) k<1><<<1, 64>>>(out, cyc);
             if (m == 2) k<2><<<1, 64>>>(out, cyc);
+            if (m == 3) k<3><<<1, 64>>>(out, cyc);
+            if (m == 4) k<4><<<1, 64>>>(out, cyc);
+            if (m == 5) k<5><<<1, 64>>>(out, cyc);
             (void)hipDeviceSynchronize();
         }
         (void)hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);
