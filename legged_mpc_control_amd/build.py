@@ -13,7 +13,7 @@ LIB = os.path.join(LIBDIR, "liblmpc.so")
 ARCH = "gfx950"
 
 SOURCES = ["lmpc_kernels.hip", "lmpc_prep.hip", "lmpc_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
-HEADERS = ["lmpc_device.h", "lmpc_common.h"]
+HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h"]
 
 
 def hipcc() -> str:

@@ -1,0 +1,186 @@
+// lmpc_kernel_common.h -- device helpers shared by the two QP kernels (lmpc_kernels.hip: the
+// Riccati path; lmpc_dense.hip: the condensed dense path): wave-scope LDS ordering, DPP wave
+// reductions, fp64 reciprocal / rsqrt with Newton refinement, the friction-pyramid rows
+// (ConvexQPSolver.cpp:131-172) and the per-leg null-space basis of the active-set polish.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+namespace lmpc {
+
+// One workgroup = one wavefront (blockDim 64, __launch_bounds__(64)): cross-lane exchange through LDS
+// needs only wavefront-scope ordering -- LDS operations of one wave are performed in order -- so the
+// "barrier" is a release/acquire fence pair at wavefront scope around a code-motion barrier.  Unlike
+// __syncthreads() it emits no s_waitcnt lgkmcnt(0): loads issued ahead (prefetches) stay in flight.
+constexpr int LMPC_WAVE = 64;
+#define LMPC_SYNC()                                              \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+    } while (0)
+
+// Explicit LDS address space: every shared access compiles to ds_read/ds_write
+// (a generic pointer would fall back to flat_load/flat_store).
+typedef __attribute__((address_space(3))) double ldouble;
+// Explicit global address space for the per-QP scratch (outlined functions would otherwise use flat ops).
+typedef __attribute__((address_space(1))) double gdouble;
+
+// ---- wave reductions without LDS: DPP inside 16-lane rows, readlane across the 4 rows ----
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+constexpr int DPP_QP_1032 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_QP_2301 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int DPP_ROR4 = 0x124;    // row_ror:4
+constexpr int DPP_ROR8 = 0x128;    // row_ror:8
+struct OpSum { __device__ static double f(double a, double b) { return a + b; } };
+struct OpMin { __device__ static double f(double a, double b) { return fmin(a, b); } };
+struct OpMax { __device__ static double f(double a, double b) { return fmax(a, b); } };
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v) {
+    v = Op::f(v, dpp_f64<DPP_QP_1032>(v));
+    v = Op::f(v, dpp_f64<DPP_QP_2301>(v));
+    v = Op::f(v, dpp_f64<DPP_ROR4>(v));
+    v = Op::f(v, dpp_f64<DPP_ROR8>(v));  // every lane holds its row's result
+    return Op::f(Op::f(readlane_f64(v, 0), readlane_f64(v, 16)), Op::f(readlane_f64(v, 32), readlane_f64(v, 48)));
+}
+__device__ __forceinline__ double wave_sum(double v) { return wave_reduce<OpSum>(v); }
+__device__ __forceinline__ double wave_min(double v) { return wave_reduce<OpMin>(v); }
+__device__ __forceinline__ double wave_max(double v) { return wave_reduce<OpMax>(v); }
+// sum over the 4 lanes of a stage (lanes 4q..4q+3 = legs of one stage)
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_f64<DPP_QP_1032>(v);
+    v += dpp_f64<DPP_QP_2301>(v);
+    return v;
+}
+
+// ---- friction pyramid, flat ground (ConvexQPSolver.cpp:131-172) ------------
+// rows: c0 -fx-mu fz <= 0 | c1 fx-mu fz <= 0 | c2 -fy-mu fz <= 0 | c3 fy-mu fz <= 0 | c4 fz <= fzmax
+__device__ __forceinline__ void cons_resid(const double f[3], double mu, double fzmax, double o[5]) {
+    o[0] = -f[0] - mu * f[2];
+    o[1] = f[0] - mu * f[2];
+    o[2] = -f[1] - mu * f[2];
+    o[3] = f[1] - mu * f[2];
+    o[4] = f[2] - fzmax;
+}
+__device__ __forceinline__ void cons_rowvec(int i, double mu, double c[3]) {
+    c[0] = (i == 0) ? -1.0 : (i == 1) ? 1.0 : 0.0;
+    c[1] = (i == 2) ? -1.0 : (i == 3) ? 1.0 : 0.0;
+    c[2] = (i == 4) ? 1.0 : -mu;
+}
+__device__ __forceinline__ void cons_tw(const double w[5], double mu, double o[3]) {
+    o[0] = -w[0] + w[1];
+    o[1] = -w[2] + w[3];
+    o[2] = -mu * (w[0] + w[1] + w[2] + w[3]) + w[4];
+}
+
+// M(yaw) = [c s 0; -s c 0; 0 0 1]  (ang_vel_to_rpy_rate, ConvexQPSolver.cpp:220-222)
+__device__ __forceinline__ double Myaw(double c, double s, int i, int j) {
+    if (i == 2) return j == 2 ? 1.0 : 0.0;
+    if (j == 2) return 0.0;
+    if (i == 0) return j == 0 ? c : s;
+    return j == 0 ? -s : c;
+}
+
+// 1/sqrt(x): hardware estimate + one Newton step (cheaper than the correctly-rounded sqrt + divide).
+__device__ __forceinline__ double rsq_nr(double x) {
+    // v_rsq_f64 is good to 2^-24 on gfx950 (tools/ubench/rsq_acc.hip); one Newton step -> ~4e-15
+    double y = __builtin_amdgcn_rsq(x);
+    y = y * fma(-0.5 * x * y, y, 1.5);
+    return y;
+}
+
+// 1/x to full fp64 precision: hardware estimate + two Newton steps
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    y = fma(y, fma(-x, y, 1.0), y);
+    return y;
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+
+// Null-space parametrisation of one leg-step for active set `act` (bit i = row ci):
+// f = up + T y, T columns orthonormal.  Returns true at the pyramid apex (f = 0).
+__device__ bool leg_basis(int act, double mu, double fzmax, double T[9], double up[3]) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) T[i] = 0.0;
+    up[0] = up[1] = up[2] = 0.0;
+    if ((act & 3) == 3 || (act & 12) == 12) return true;
+    double rows[3][3], bs[3];
+    int nr = 0;
+    for (int i = 0; i < 5; ++i) {
+        if (!((act >> i) & 1) || nr >= 3) continue;
+        cons_rowvec(i, mu, rows[nr]);
+        bs[nr] = (i == 4) ? fzmax : 0.0;
+        ++nr;
+    }
+    double qv[3][3];
+    for (int a = 0; a < nr; ++a) {
+        double v[3] = {rows[a][0], rows[a][1], rows[a][2]};
+        for (int b = 0; b < a; ++b) {
+            const double d = qv[b][0] * v[0] + qv[b][1] * v[1] + qv[b][2] * v[2];
+            v[0] -= d * qv[b][0];
+            v[1] -= d * qv[b][1];
+            v[2] -= d * qv[b][2];
+        }
+        const double n = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        qv[a][0] = v[0] * n;
+        qv[a][1] = v[1] * n;
+        qv[a][2] = v[2] * n;
+    }
+    {
+        double beta[3] = {0.0, 0.0, 0.0};
+        for (int a = 0; a < nr; ++a) {
+            double s = bs[a];
+            for (int b = 0; b < a; ++b)
+                s -= (rows[a][0] * qv[b][0] + rows[a][1] * qv[b][1] + rows[a][2] * qv[b][2]) * beta[b];
+            const double diag = rows[a][0] * qv[a][0] + rows[a][1] * qv[a][1] + rows[a][2] * qv[a][2];
+            beta[a] = s / diag;
+        }
+        for (int a = 0; a < nr; ++a)
+            for (int i = 0; i < 3; ++i) up[i] += beta[a] * qv[a][i];
+    }
+    if (nr == 0) {
+        T[0] = T[4] = T[8] = 1.0;
+    } else if (nr == 1) {
+        const double* n = qv[0];
+        double e[3] = {0.0, 0.0, 0.0};
+        if (fabs(n[0]) < 0.9) e[0] = 1.0;
+        else e[1] = 1.0;
+        const double d = n[0] * e[0] + n[1] * e[1] + n[2] * e[2];
+        double t1[3] = {e[0] - d * n[0], e[1] - d * n[1], e[2] - d * n[2]};
+        const double in = 1.0 / sqrt(t1[0] * t1[0] + t1[1] * t1[1] + t1[2] * t1[2]);
+        t1[0] *= in;
+        t1[1] *= in;
+        t1[2] *= in;
+        const double t2[3] = {n[1] * t1[2] - n[2] * t1[1], n[2] * t1[0] - n[0] * t1[2], n[0] * t1[1] - n[1] * t1[0]};
+        for (int i = 0; i < 3; ++i) {
+            T[i * 3 + 0] = t1[i];
+            T[i * 3 + 1] = t2[i];
+        }
+    } else if (nr == 2) {
+        double t[3] = {qv[0][1] * qv[1][2] - qv[0][2] * qv[1][1], qv[0][2] * qv[1][0] - qv[0][0] * qv[1][2],
+                       qv[0][0] * qv[1][1] - qv[0][1] * qv[1][0]};
+        const double in = 1.0 / sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        for (int i = 0; i < 3; ++i) T[i * 3 + 0] = t[i] * in;
+    }
+    return false;
+}
+
+}  // namespace lmpc
