@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -16,6 +17,8 @@
 namespace lmpc {
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                      int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, hipStream_t stream);
+hipError_t launch_dense(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                        int batch, double* grf, int32_t* status, int32_t* iters, hipStream_t stream);
 hipError_t launch_records(const lmpc_command* cmd, int batch, int H, double dt, double* rec, uint8_t* contact,
                           hipStream_t stream);
 hipError_t launch_synth(const lmpc_synth_cfg& cfg, uint64_t seed, int64_t first, int count, lmpc_command* cmd,
@@ -120,6 +123,9 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     lmpc_options_default(&o);
     fill_options(c->prm, &o);
     c->prm.H = horizon;
+    // condensed dense path for H <= DENSE_MAX_H (LMPC_DENSE=0 forces the Riccati path, for A/B checks)
+    const char* dn = std::getenv("LMPC_DENSE");
+    c->prm.dense = (horizon <= lmpc::DENSE_MAX_H && !(dn && dn[0] == '0')) ? 1 : 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return LMPC_ERR_DEVICE;
@@ -200,8 +206,11 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
         const int rc = lmpc_reserve(c, batch);
         if (rc != LMPC_OK) return rc;
     }
-    const hipError_t e =
-        lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch, s);
+    hipError_t e = hipSuccess;
+    if (c->prm.dense)  // condensed dense kernel first; the Riccati kernel then skips the QPs it solved
+        e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, s);
+    if (e == hipSuccess)
+        e = lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
 }

@@ -22,7 +22,10 @@ struct DevParams {
     int max_iter;      // IPM iteration cap (per attempt)
     int max_rounds;    // polish rounds per attempt
     int max_attempts;  // IPM+polish attempts (tol_mu tightened x1e-3 per attempt)
+    int dense;         // 1: QPs with 1..DENSE_MAX_LS stance leg-steps go to the condensed dense kernel
 };
+constexpr int DENSE_MAX_LS = 20;  // 5 leg-steps per 16-wide tile x 4 tiles (lmpc_dense.hip)
+constexpr int DENSE_MAX_H = 16;   // the dense path's per-step LDS arrays
 
 // LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
 constexpr int LDS_FIXED_DOUBLES = 464;  // per-QP matrices and buffers

@@ -802,6 +802,11 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     if (qp >= batch) return;
     const int lane = threadIdx.x;
     const int H = prm.H;
+    if (prm.dense) {  // QPs with 1..DENSE_MAX_LS stance leg-steps are solved by lmpc_dense_kernel (H <= 16 here)
+        const bool stl = lane < 4 * H && contact[(size_t)qp * 4 * H + lane] != 0;
+        const int n = __popcll(__ballot(stl));
+        if (n >= 1 && n <= DENSE_MAX_LS) return;
+    }
     const int RL = 33 + 12 * H;
     const Smem S = carve(lmpc_smem, H);
     ldouble* const tf = S.st + SK * H;  // TERRAIN only: R_j (9 each, row-major) | R_j' diag(r_j) R_j packed (6 each)

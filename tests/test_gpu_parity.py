@@ -331,3 +331,45 @@ def test_terrain_rejects_bad_normals():
         s.solve(rec, con, normals=bad)
     with pytest.raises(ValueError):
         s.solve(rec, con, normals=np.zeros((4, 3)))
+
+
+# ---------------------------------------------------------------------------
+# the two device paths: condensed dense kernel (<= 20 stance leg-steps, H <= 16) and Riccati kernel
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("cid", [2, 4])
+def test_dense_and_riccati_paths_agree(cid, monkeypatch):
+    """Every config-2 QP (and the trot-like config-4 QPs) runs on the dense path by default; with
+    LMPC_DENSE=0 the same QPs run on the Riccati path.  Both must give the oracle's optimum."""
+    p, H, rec, con = synth.config_batch(cid, count=512, first_index=777)
+    nrm = synth.config_normals(cid, count=512, first_index=777)
+    nls = con.sum((1, 2))
+    assert np.any(nls <= 20) and (cid == 4 or np.all(nls <= 20))
+    monkeypatch.setenv("LMPC_DENSE", "1")
+    gd, sd, itd = BatchedConvexQPSolver(p, H, max_batch=512).solve(rec, con, normals=nrm)
+    monkeypatch.setenv("LMPC_DENSE", "0")
+    gr, sr, itr = BatchedConvexQPSolver(p, H, max_batch=512).solve(rec, con, normals=nrm)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8, normals=nrm)
+    assert fails == 0 and np.all(sd == 0) and np.all(sr == 0)
+    assert rel_err(gd, ref) <= TOL_REGRESS and rel_err(gr, ref) <= TOL_REGRESS
+    assert rel_err(gd, gr) <= 1e-8
+    # same Newton systems, so the same iteration counts on both paths
+    assert np.mean(np.abs((itd & 0xFFFF) - (itr & 0xFFFF))) < 0.05
+
+
+def test_dense_path_edge_cases(monkeypatch):
+    """Dense-path QPs with fewer than 20 stance leg-steps (partly padded tiles), a single stance
+    leg-step, and the all-swing QP (left to the Riccati kernel)."""
+    monkeypatch.setenv("LMPC_DENSE", "1")
+    p, H, rec, con = synth.config_batch(2, count=8, first_index=31)
+    con = con.copy()
+    con[0, :, :] = 0; con[0, 0, 1] = 1          # one stance leg-step
+    con[1, 5:, :] = 0                           # 10 stance leg-steps (tiles 2-3 empty)
+    con[2, :, :] = 0                            # all swing -> zeros (Riccati kernel)
+    con[3, :, 0] = 1; con[3, :, 1:] = 0         # one leg in stance all horizon
+    con[4, 0:4, :] = 1                          # 16 + ... stance: > 20 -> Riccati
+    s = BatchedConvexQPSolver(p, H, max_batch=8)
+    g, st, it = s.solve(rec, con)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=4)
+    assert fails == 0 and np.all(st == 0), st
+    assert rel_err(g, ref) <= TOL_REGRESS
+    assert np.all(g[2] == 0.0)

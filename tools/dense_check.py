@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Dev tool (GPU): the condensed dense path vs the Riccati path vs the oracle, and their kernel times.
+LMPC_DENSE is read at lmpc_create, so each solver below picks its path from the environment."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+torch.cuda.init()
+from legged_mpc_control_amd import BatchedConvexQPSolver, synth  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def solver(p, H, B, dense):
+    os.environ["LMPC_DENSE"] = "1" if dense else "0"
+    return BatchedConvexQPSolver(p, H, B)
+
+
+def main():
+    for cid, cnt in ((2, 256), (4, 256), (1, 1)):
+        p, H, rec, con = synth.config_batch(cid, count=cnt)
+        nrm = synth.config_normals(cid, count=cnt)
+        ref, _, _ = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8, normals=nrm)
+        for dense in (True, False):
+            g, st, it = solver(p, H, cnt, dense).solve(rec, con, normals=nrm)
+            err = np.max(np.abs(g - ref) / np.maximum(1.0, np.abs(ref)))
+            nls = (con.sum((1, 2)))
+            print(f"config {cid} dense={dense}: max err {err:.2e} status {np.bincount(st, minlength=3)} "
+                  f"ipm {np.mean(it & 0xffff):.2f} rounds {np.mean(it >> 16):.2f} "
+                  f"(dense-eligible {(nls <= 20).sum()}/{cnt})", flush=True)
+            if err > 1e-6:
+                bad = np.argsort(-np.max(np.abs(g - ref).reshape(cnt, -1), 1))[:3]
+                for b in bad:
+                    print("   worst", b, "nls", nls[b], "err", np.max(np.abs(g[b] - ref[b])), "status", st[b], "it", it[b] & 0xffff, it[b] >> 16)
+    # timing, config 2 full batch
+    p, H, rec, con = synth.config_batch(2)
+    dev = torch.device("cuda", 0)
+    for dense in (True, False, True):
+        s = solver(p, H, len(rec), dense)
+        d = [torch.from_numpy(rec).to(dev), torch.from_numpy(con).to(dev),
+             torch.empty((len(rec), H, 12), dtype=torch.float64, device=dev),
+             torch.empty(len(rec), dtype=torch.int32, device=dev), torch.empty(len(rec), dtype=torch.int32, device=dev)]
+        stream = torch.cuda.Stream(dev)
+        for _ in range(3):
+            s.solve_device(*d, stream=stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            s.solve_device(*d, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        print(f"config 2 B=1024 dense={dense}: {e0.elapsed_time(e1) / 20:.4f} ms per solve", flush=True)
+
+
+
+
+def stamps():
+    """Per-phase cycles of the dense kernel (needs the -DLMPC_STAMPS library: build.build_stamps())."""
+    import ctypes
+
+    from legged_mpc_control_amd import _native as N
+    p, H, rec, con = synth.config_batch(2)
+    s = solver(p, H, len(rec), True)
+    g, st, it = s.solve(rec, con)
+    L = N.lib()
+    L.lmpc_debug_dense_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = np.zeros((1024, 8), dtype=np.uint64)
+    n = L.lmpc_debug_dense_stamps(buf.ctypes.data, 1024)
+    names = ["prologue", "condense", "leg+rhs", "M tiles (ipm)", "factor (MFMA part)", "solve", "diag tiles", "M tiles (polish)"]
+    tot = buf[:n, :8].sum(1).astype(float)
+    print(f"dense config 2: mean cycles/QP {tot.mean():.0f} (ipm {np.mean(it & 0xffff):.2f} rounds {np.mean(it >> 16):.2f})")
+    for i, nm in enumerate(names):
+        v = buf[:n, i].astype(float).mean()
+        print(f"  {nm:20s} {v:10.0f} ({100 * v / tot.mean():5.1f}%)")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "stamps":
+        from legged_mpc_control_amd import build as B
+        os.environ["LMPC_LIB"] = B.build_stamps()
+        stamps()
+    else:
+        main()
