@@ -120,7 +120,10 @@ int lmpc_solve_batch(lmpc_ctx* ctx, const double* rec, const uint8_t* contact, i
                      double* grf, int32_t* status, int32_t* iters);
 
 /* Device buffers (already resident in HBM), asynchronous on `stream`
- * (a hipStream_t; NULL = the context's own stream). status/iters may be NULL. */
+ * (a hipStream_t; NULL = HIP's null stream, which is ordered with every blocking stream, e.g.
+ * PyTorch's default stream -- the context's own stream is non-blocking and is used only by the
+ * host-pointer entry points). Every `void* stream` of this header has this meaning.
+ * status/iters may be NULL. */
 int lmpc_solve_batch_device(lmpc_ctx* ctx, const double* d_rec, const uint8_t* d_contact,
                             int batch, double* d_grf, int32_t* d_status, int32_t* d_iters,
                             void* stream);

@@ -201,7 +201,7 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
                                int batch, double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_rec || !d_contact || !d_grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     if ((size_t)batch > c->scratch_qps) {
         const int rc = lmpc_reserve(c, batch);
         if (rc != LMPC_OK) return rc;
@@ -268,7 +268,7 @@ int lmpc_build_records_device(lmpc_ctx* c, const lmpc_command* d_cmd, int batch,
                               void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_cmd || !d_rec || !d_contact))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     return launch_rc(lmpc::launch_records(d_cmd, batch, c->H, c->prm.dt, d_rec, d_contact, s));
 }
 
@@ -276,7 +276,7 @@ int lmpc_solve_commands_device(lmpc_ctx* c, const lmpc_command* d_cmd, const dou
                                double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_cmd || !d_grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     if ((size_t)batch > c->cmd_qps) {
         if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
         (void)hipDeviceSynchronize();  // the old buffers may still be read by queued work
@@ -299,7 +299,7 @@ int lmpc_synth_commands_device(lmpc_ctx* c, const lmpc_synth_cfg* cfg, uint64_t 
                                lmpc_command* d_cmd, void* stream) {
     if (!c || !cfg || count < 0 || (count > 0 && !d_cmd)) return LMPC_ERR_ARG;
     if (count == 0) return LMPC_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     return launch_rc(lmpc::launch_synth(*cfg, seed, first_index, count, d_cmd, s));
 }
 
@@ -308,7 +308,7 @@ int lmpc_synth_normals_device(lmpc_ctx* c, uint64_t seed, int64_t first_index, i
     if (!c || count < 0 || (count > 0 && !d_normals) || !(theta_max >= 0.0) || theta_max >= 1.5707963267948966)
         return LMPC_ERR_ARG;
     if (count == 0) return LMPC_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     return launch_rc(lmpc::launch_normals(seed, first_index, count, theta_max, d_normals, s));
 }
 
@@ -316,7 +316,7 @@ int lmpc_grf_to_torque_device(lmpc_ctx* c, const lmpc_leg_kin* k, const double* 
                               const double* d_grf, int batch, double* d_tau, void* stream) {
     if (!c || !k || batch < 0 || (batch > 0 && (!d_rec || !d_joint_pos || !d_grf || !d_tau))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     return launch_rc(lmpc::launch_torque(*k, d_rec, d_joint_pos, d_grf, batch, c->H, d_tau, s));
 }
 

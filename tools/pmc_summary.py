@@ -4,7 +4,7 @@ profiles/<tag>/{c2,c4}_kernel_stats.csv, pmc_per_dispatch.json, pmc_calibration.
 profiles/pmc_traffic.json (bytes per launch for bench.py's roofline.traffic).
 
 Calibration (tools/ubench/pmc_cal.hip, 512 MiB past the Infinity Cache): for 8-byte-per-lane
-coalesced accesses, the access width lmpc_qp_kernel uses, FETCH_SIZE reports half the bytes read
+coalesced accesses, the access width the solve kernels use, FETCH_SIZE reports half the bytes read
 and WRITE_SIZE reports the bytes written exactly.  The read factor is applied to FETCH_SIZE."""
 import csv
 import json
@@ -23,7 +23,10 @@ def rows(name):
     return list(csv.DictReader(open(os.path.join(SRC, name, f"{name}_counter_collection.csv"))))
 
 
-def per_kernel(name, kern="lmpc_qp_kernel"):
+SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_qp_kernel")  # one solve launch = both (the second skips the first's QPs)
+
+
+def per_kernel(name, kern):
     r = [x for x in rows(name) if kern in x["Kernel_Name"]]
     return [float(x["Counter_Value"]) for x in r], [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in r]
 
@@ -44,11 +47,17 @@ def main():
     per = {}
     traffic = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     for c, wl, qps in (("2", "go1_trot_h10_b1024", 1024), ("4", "go1_mixed_h10_b65536+terrain", 65536)):
-        f, fd = per_kernel(f"f{c}")
-        w, wd = per_kernel(f"w{c}")
-        fb, wb = st.mean(f) * 1024 * read_factor, st.mean(w) * 1024 * write_factor
-        per[wl] = dict(fetch_kib_raw=f, write_kib_raw=w, fetch_bytes=fb, write_bytes=wb,
-                       dispatch_ns_fetch_pass=fd, dispatch_ns_write_pass=wd)
+        fb = wb = 0.0
+        per[wl] = {}
+        for kern in SOLVE_KERNELS:
+            f, fd = per_kernel(f"f{c}", kern)
+            w, wd = per_kernel(f"w{c}", kern)
+            if not f:
+                continue
+            kf, kw = st.mean(f) * 1024 * read_factor, st.mean(w) * 1024 * write_factor
+            fb, wb = fb + kf, wb + kw
+            per[wl][kern] = dict(fetch_kib_raw=f, write_kib_raw=w, fetch_bytes=kf, write_bytes=kw,
+                                 dispatch_ns_fetch_pass=fd, dispatch_ns_write_pass=wd)
         traffic[wl] = {
             "bytes_per_launch": fb + wb,
             "bytes_per_qp": (fb + wb) / qps,
@@ -56,7 +65,7 @@ def main():
             "write_bytes": wb,
             "source": f"profiles/{TAG}/pmc_per_dispatch.json",
             "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py "
-                      f"(config {c}, --no-cpu); per-dispatch mean of lmpc_qp_kernel; FETCH_SIZE x {read_factor:.3f}, "
+                      f"(config {c}, --no-cpu); per-dispatch means of lmpc_dense_kernel + lmpc_qp_kernel; FETCH_SIZE x {read_factor:.3f}, "
                       f"WRITE_SIZE x {write_factor:.3f} from profiles/{TAG}/pmc_calibration.json",
         }
     json.dump(per, open(os.path.join(DST, "pmc_per_dispatch.json"), "w"), indent=1)
