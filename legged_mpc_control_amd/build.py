@@ -12,8 +12,8 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "liblmpc.so")
 ARCH = "gfx950"
 
-SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_prep.hip", "lmpc_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
-HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h"]
+SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
+HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h"]
 
 
 def hipcc() -> str:

@@ -16,7 +16,10 @@
 
 namespace lmpc {
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
-                     int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, hipStream_t stream);
+                     int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, const uint8_t* done,
+                     hipStream_t stream);
+hipError_t launch_gi(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                     int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
 hipError_t launch_dense(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                         int batch, double* grf, int32_t* status, int32_t* iters, hipStream_t stream);
 hipError_t launch_records(const lmpc_command* cmd, int batch, int H, double dt, double* rec, uint8_t* contact,
@@ -42,6 +45,7 @@ struct lmpc_ctx {
     int32_t* d_status = nullptr;
     int32_t* d_iters = nullptr;
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
+    uint8_t* d_done = nullptr;    // per-QP flag: solved by the GI kernel (else the Riccati kernel solves it)
     size_t scratch_qps = 0;
     double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
     uint8_t* d_ccon = nullptr;
@@ -88,7 +92,9 @@ void free_bufs(lmpc_ctx* c) {
     (void)hipFree(c->d_status);
     (void)hipFree(c->d_iters);
     (void)hipFree(c->d_scratch);
+    (void)hipFree(c->d_done);
     c->d_scratch = nullptr;
+    c->d_done = nullptr;
     c->scratch_qps = 0;
     (void)hipFree(c->d_crec);
     (void)hipFree(c->d_ccon);
@@ -123,9 +129,16 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     lmpc_options_default(&o);
     fill_options(c->prm, &o);
     c->prm.H = horizon;
-    // condensed dense path for H <= DENSE_MAX_H (LMPC_DENSE=0 forces the Riccati path, for A/B checks)
+    // condensed dense path for H <= DENSE_MAX_H: the interior point (lmpc_dense.hip) by default;
+    // LMPC_DENSE=gi selects the dual active set (lmpc_gi.hip), LMPC_DENSE=0 the Riccati kernel for every
+    // QP (A/B checks).  The choice is fixed per context, never per launch, so a QP's answer does not
+    // depend on the batch it is solved in.  Why the interior point is the default: DESIGN.md 4b.
     const char* dn = std::getenv("LMPC_DENSE");
-    c->prm.dense = (horizon <= lmpc::DENSE_MAX_H && !(dn && dn[0] == '0')) ? 1 : 0;
+    c->prm.dense = horizon > lmpc::DENSE_MAX_H || (dn && dn[0] == '0') ? 0 : (dn && dn[0] == 'g') ? 2 : 1;
+    {
+        const char* gm = std::getenv("LMPC_GI_MAX_STEPS");  // test hook: exercise the hand-over to the Riccati kernel
+        c->prm.gi_max_steps = gm ? std::atoi(gm) : 240;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return LMPC_ERR_DEVICE;
@@ -186,11 +199,16 @@ int lmpc_reserve(lmpc_ctx* c, int batch) {
         (void)hipStreamSynchronize(c->stream);
         (void)hipDeviceSynchronize();
         (void)hipFree(c->d_scratch);
+        (void)hipFree(c->d_done);
         c->d_scratch = nullptr;
+        c->d_done = nullptr;
         c->scratch_qps = 0;
     }
-    if (hipMalloc(&c->d_scratch, (size_t)batch * lmpc::scratch_doubles_per_qp(c->H) * sizeof(double)) != hipSuccess) {
+    if (hipMalloc(&c->d_scratch, (size_t)batch * lmpc::scratch_doubles_per_qp(c->H) * sizeof(double)) != hipSuccess ||
+        hipMalloc(&c->d_done, (size_t)batch) != hipSuccess) {
+        (void)hipFree(c->d_scratch);
         c->d_scratch = nullptr;
+        c->d_done = nullptr;
         return LMPC_ERR_ALLOC;
     }
     c->scratch_qps = (size_t)batch;
@@ -207,10 +225,14 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
         if (rc != LMPC_OK) return rc;
     }
     hipError_t e = hipSuccess;
-    if (c->prm.dense)  // condensed dense kernel first; the Riccati kernel then skips the QPs it solved
+    // condensed dense kernel first; the Riccati kernel then skips the QPs it solved
+    if (c->prm.dense == 2)
+        e = lmpc::launch_gi(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
+    else if (c->prm.dense == 1)
         e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, s);
     if (e == hipSuccess)
-        e = lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch, s);
+        e = lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch,
+                            c->prm.dense == 2 ? c->d_done : nullptr, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
 }

@@ -1,0 +1,516 @@
+// lmpc_dense_common.h -- the condensed dense path's shared device code (gfx950), used by both
+// dense-path kernels: lmpc_dense.hip (interior point + active-set polish on the condensed QP) and
+// lmpc_gi.hip (dual active-set / Goldfarb-Idnani on the condensed QP).
+//
+// Variables of the condensed QP are the stance forces only, laid out 5 leg-steps (15 variables + 1
+// padding slot) per 16-wide tile, so every 3x3 leg block sits inside one tile and N <= 64 fits 4x4
+// tiles.  The Hessian H is kept in LDS as its upper tiles in the MFMA accumulator layout
+// (lane l, register i <-> row (l>>4)+4i, column l&15).  Padding / unused slots carry identity rows.
+//
+// Prologue (record load, I_w^-1, B = G0, yaw cos/sin, per-leg R blocks; ConvexQPSolver.cpp:198-228)
+// and condensation (ConvexQPSolver.cpp:254-313 in condensed form):
+//   free response  c_{m+1} = A_m c_m - g dt e11,  c_0 = x0
+//   adjoint        mu_m = Q (c_m - xref_{m-1}) + A_m' mu_{m+1}          -> g_i = B' mu_{i+1}
+//   cost-to-go     P~_H = Q,  P~_m = Q + A_m' P~_{m+1} A_m              (fp64 MFMA, 12x12)
+//   Hessian        H[i][j] = B' (A_j ... A_{i+1})' P~_{j+1} B  (i <= j), + R on the diagonal blocks,
+//                  one column per lane: L = P~_{j+1} B e_c, then L <- A_{i+1}' L down the steps.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "lmpc/lmpc.h"
+#include "lmpc_device.h"
+#include "lmpc_kernel_common.h"
+
+namespace lmpc {
+
+constexpr int DN_TILE = 256;  // doubles per 16x16 tile
+size_t dense_lds_bytes(int H);  // host: dynamic LDS of the dense-path carve (lmpc_dense.hip)
+
+// packed index of the upper tile (r, c), r <= c < 4
+__device__ __forceinline__ constexpr int tix(int r, int c) { return r * 4 - r * (r - 1) / 2 + (c - r); }
+// index of the off-diagonal tile (a, b), a < b < 4
+__device__ __forceinline__ constexpr int uix(int a, int b) { return a == 0 ? b - 1 : a == 1 ? b + 1 : 5; }
+// element (r, c) of a tile in accumulator order (lane (r&3)*16 + c, register r>>2)
+__device__ __forceinline__ int toff(int r, int c) { return (r >> 2) * 64 + (r & 3) * 16 + c; }
+// variable of leg-step b, component a
+__device__ __forceinline__ int vidx(int b, int a) { return 16 * (b / 5) + 3 * (b % 5) + a; }
+// packed symmetric 3x3 [xx xy xz yy yz zz]
+__device__ __forceinline__ int sym3(int p, int q) {
+    const int lo = p < q ? p : q, hi = p < q ? q : p;
+    return lo == 0 ? hi : lo == 1 ? 2 + hi : 5;
+}
+
+// acc += X' Y on 16x16 tiles (4 MFMAs); sub: acc -= X' Y
+__device__ __forceinline__ d4 tprod(const d4& X, const d4& Y, d4 acc) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc = MFMA64(X[kk], Y[kk], acc);
+    return acc;
+}
+__device__ __forceinline__ d4 tprod_sub(const d4& X, const d4& Y, d4 acc) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc = MFMA64(-X[kk], Y[kk], acc);
+    return acc;
+}
+
+typedef __attribute__((address_space(3))) int lint;
+
+// sum over the 16 lanes of each DPP row (every lane gets its row's total)
+__device__ __forceinline__ double row_sum(double v) {
+    v += dpp_f64<DPP_QP_1032>(v);
+    v += dpp_f64<DPP_QP_2301>(v);
+    v += dpp_f64<DPP_ROR4>(v);
+    v += dpp_f64<DPP_ROR8>(v);
+    return v;
+}
+
+struct DSmem {
+    ldouble* hdr;   // 40: x0(12) R(9) feet(12)
+    ldouble* G0;    // 72: B rows 6-11 (terrain: G0 blkdiag(R_j))
+    ldouble* rb;    // 24: per-leg input Hessian block, packed symmetric
+    ldouble* tf;    // 36: terrain frames R_j (row-major)
+    ldouble* cs;    // 2H
+    ldouble* xr;    // 12H
+    ldouble* em;    // 12H: Q (c_{m+1} - xref_m)
+    ldouble* Ht;    // 10 tiles: upper tiles of H
+    ldouble* gv;    // 64: condensed gradient
+    ldouble* vec;   // 64: right-hand side in / solution out
+    ldouble* vec2;  // 64: matvec operand / result
+    ldouble* blk;   // 180: per-leg-step 3x3 block (D in the IPM, T in the polish)
+    ldouble* act;   // 20: 1 = leg-step coupled (T != 0)
+    ldouble* lup;   // 60: polish particular solution up per leg-step (kept out of registers)
+    ldouble* lua;   // 60: predictor step u_aff per leg-step
+    ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | el(272) PNL(96) L^-1(272)
+    lint* lsm;      // 20: stance leg-step b -> 4k + j
+    lint* fb;       // H+1: first stance leg-step of step k
+};
+constexpr int DN_EL = 16 * 17;                // staging of one 16x16 tile, column stride 17
+constexpr int DN_SCR_MIN = DN_EL + 96 + DN_EL;  // el | PNL | L^-1
+
+__device__ __forceinline__ DSmem dcarve(double* sm, int H) {
+    DSmem s;
+    ldouble* p = (ldouble*)sm;
+    s.hdr = p; p += 40;
+    s.G0 = p; p += 72;
+    s.rb = p; p += 24;
+    s.tf = p; p += 36;
+    s.Ht = p; p += 10 * DN_TILE;
+    s.gv = p; p += 64;
+    s.vec = p; p += 64;
+    s.vec2 = p; p += 64;
+    s.blk = p; p += 180;
+    s.act = p; p += 20;
+    s.lup = p; p += 60;
+    s.lua = p; p += 60;
+    s.cs = p; p += 2 * H;
+    s.xr = p; p += 12 * H;
+    s.em = p; p += 12 * H;
+    s.scr = p; p += (72 * H > DN_SCR_MIN ? 72 * H : DN_SCR_MIN);
+    lint* ip = (lint*)p;
+    s.lsm = ip;
+    s.fb = ip + 20;
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// Condensation: em, g, P~, H (see the header comment).  All lanes; lane v = variable v.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem& S, int H, int nls, int lane) {
+    const double dt = prm.dt;
+    // ---- free response and adjoint (every lane redundantly: no exchange needed) ----
+    {
+        double x[12];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) x[r] = S.hdr[r];
+        for (int m = 0; m < H; ++m) {
+            const double ck = S.cs[2 * m], sk = S.cs[2 * m + 1];
+            const double x6 = x[6], x7 = x[7], x8 = x[8];
+            x[0] += dt * (ck * x6 + sk * x7);
+            x[1] += dt * (-sk * x6 + ck * x7);
+            x[2] += dt * x8;
+            x[3] += dt * x[9];
+            x[4] += dt * x[10];
+            x[5] += dt * x[11];
+            x[11] -= prm.grav * dt;
+            if (lane < 12) {
+                double xl = x[0];
+#pragma unroll
+                for (int r = 1; r < 12; ++r) xl = (lane == r) ? x[r] : xl;
+                S.em[12 * m + lane] = prm.q[lane] * (xl - S.xr[12 * m + lane]);
+            }
+        }
+    }
+    // variable of this lane
+    const int vt = lane >> 4, vw = lane & 15;
+    const int vb = 5 * vt + vw / 3, va = vw % 3;
+    const bool vvalid = vw < 15 && vb < nls;
+    LMPC_SYNC();
+    int vk = 0, vj = 0;
+    if (vvalid) {
+        const int id = S.lsm[vb];
+        vk = id >> 2;
+        vj = id & 3;
+    }
+    const int vc = 3 * vj + va;
+    {
+        double mu[12];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) mu[r] = 0.0;
+        double gval = 0.0;
+        for (int m = H; m >= 1; --m) {
+            if (m < H) {  // mu <- A_m' mu
+                const double ck = S.cs[2 * m], sk = S.cs[2 * m + 1];
+                const double m0 = mu[0], m1 = mu[1], m2 = mu[2];
+                mu[6] += dt * (ck * m0 - sk * m1);
+                mu[7] += dt * (sk * m0 + ck * m1);
+                mu[8] += dt * m2;
+                mu[9] += dt * mu[3];
+                mu[10] += dt * mu[4];
+                mu[11] += dt * mu[5];
+            }
+#pragma unroll
+            for (int r = 0; r < 12; ++r) mu[r] += S.em[12 * (m - 1) + r];
+            if (vvalid && vk + 1 == m) {
+                double gs = 0.0;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) gs += S.G0[q * 12 + vc] * mu[6 + q];
+                gval = gs;
+            }
+        }
+        S.gv[lane] = gval;
+    }
+    // ---- P~ recursion on the matrix cores; store P~_m[:, 6:12] for m = 1..H ----
+    {
+        const int lc = lane & 15, lr = lane >> 4;
+        d4 P;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = lr + 4 * i;
+            P[i] = (r == lc && r < 12) ? prm.q[r < 12 ? r : 0] : 0.0;
+        }
+        const d4 Qd = P;
+        double nc[2], ns[2], n1[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int r = 4 * kk + lr, c = lc;
+            nc[kk] = ns[kk] = n1[kk] = 0.0;
+            if (r < 3 && c >= 6 && c < 9) {
+                const int j = c - 6;
+                if (r == 0) { nc[kk] = (j == 0) ? dt : 0.0; ns[kk] = (j == 1) ? dt : 0.0; }
+                if (r == 1) { ns[kk] = (j == 0) ? -dt : 0.0; nc[kk] = (j == 1) ? dt : 0.0; }
+                if (r == 2) n1[kk] = (j == 2) ? dt : 0.0;
+            }
+            if (r >= 3 && r < 6 && c == r + 6) n1[kk] = dt;
+        }
+        for (int m = H; m >= 1; --m) {
+            if (m < H) {
+                const double ck = S.cs[2 * m], sk = S.cs[2 * m + 1];
+                double nh[2];
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) nh[kk] = fma(nc[kk], ck, fma(ns[kk], sk, n1[kk]));
+                d4 PA = P;
+                PA = MFMA64(P[0], nh[0], PA);
+                PA = MFMA64(P[1], nh[1], PA);
+                d4 Pn = Qd + PA;
+                Pn = MFMA64(nh[0], PA[0], Pn);
+                Pn = MFMA64(nh[1], PA[1], Pn);
+                P = Pn;
+            }
+            if (lc >= 6 && lc < 12) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const int r = lr + 4 * i;
+                    S.scr[72 * (m - 1) + 6 * r + (lc - 6)] = P[i];
+                }
+            }
+        }
+    }
+    // ---- H: zero tiles, identity on padding / unused slots, then one column per lane ----
+#pragma unroll 4
+    for (int e = lane; e < 10 * DN_TILE; e += 64) S.Ht[e] = 0.0;
+    LMPC_SYNC();
+    {
+        // identity on the diagonal of padding and unused variables (lane v = variable v)
+        if (!vvalid) S.Ht[tix(vt, vt) * DN_TILE + toff(vw, vw)] = 1.0;
+    }
+    if (vvalid) {
+        double L[12];
+        const ldouble* Pt = S.scr + 72 * vk;  // P~_{k+1}
+        double gc[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) gc[q] = S.G0[q * 12 + vc];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) {
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc = fma(Pt[6 * r + q], gc[q], acc);
+            L[r] = acc;
+        }
+        const int v = lane;
+        for (int i = vk; i >= 0; --i) {
+            if (i < vk) {  // L <- A_{i+1}' L
+                const double ck = S.cs[2 * (i + 1)], sk = S.cs[2 * (i + 1) + 1];
+                const double l0 = L[0], l1 = L[1], l2 = L[2];
+                L[6] += dt * (ck * l0 - sk * l1);
+                L[7] += dt * (sk * l0 + ck * l1);
+                L[8] += dt * l2;
+                L[9] += dt * L[3];
+                L[10] += dt * L[4];
+                L[11] += dt * L[5];
+            }
+            const int b0 = S.fb[i], b1 = S.fb[i + 1];
+            for (int bp = b0; bp < b1; ++bp) {
+                const int jp = S.lsm[bp] & 3;
+#pragma unroll
+                for (int ap = 0; ap < 3; ++ap) {
+                    const int cp = 3 * jp + ap;
+                    double val = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+                    if (bp == vb) val += S.rb[6 * vj + sym3(ap, va)];
+                    const int vp = vidx(bp, ap);
+                    const int tp = vp >> 4;
+                    if (tp <= vt) S.Ht[tix(tp, vt) * DN_TILE + toff(vp & 15, vw)] = val;
+                    if (tp == vt && i < vk) S.Ht[tix(vt, vt) * DN_TILE + toff(vw, vp & 15)] = val;
+                }
+            }
+        }
+    }
+    LMPC_SYNC();
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal tile: U_bb^-1 (Ui, = L^-T) and its transpose (UiT, = L^-1) of M_bb = L L'.
+// Block Cholesky by leg blocks (3x3 pivots) on [M_bb | I], one column per lane (lanes 0-31),
+// decoupled identity blocks (unused / padding / apex legs) skipped.  amask: coupled blocks (bits 0-4).
+// ---------------------------------------------------------------------------
+struct DiagInv {
+    d4 ui, uit;
+};
+// Outlined (one call site): the elimination gets the caller-saved registers to itself instead of
+// competing with the factor tiles and the leg state that are live around it.
+static __device__ __attribute__((noinline)) DiagInv diag_inverse(ldouble* scr, d4 M, int amask, int lane) {
+    // column-major staging with an odd column stride (17 doubles): a wave's 16 columns fall on
+    // distinct LDS banks (a stride of 16 puts them on two banks: 8-way conflicts)
+    ldouble* el = scr;
+    ldouble* PNL = scr + DN_EL;
+    ldouble* li = scr + DN_EL + 96;
+    const int lc = lane & 15, lr = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) el[lc * 17 + lr + 4 * i] = M[i];
+    LMPC_SYNC();
+    double a[16];
+    {
+        const ldouble* src = el + 17 * (lane < 16 ? lane : 0);
+        const double keep = (lane < 16) ? 1.0 : 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = fma(src[r], keep, (r == lane - 16) ? 1.0 : 0.0);
+    }
+    if (amask) {
+        const int b0 = __builtin_ctz(amask);
+        if (lane >= 3 * b0 && lane < 3 * b0 + 3) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) PNL[(lane - 3 * b0) * 16 + r] = a[r];
+        }
+    }
+    int par = 0;
+#pragma unroll
+    for (int blk = 0; blk < 5; ++blk) {
+        if (!((amask >> blk) & 1)) continue;
+        const int o = 3 * blk;
+        const ldouble* pnl = PNL + par * 48;
+        LMPC_SYNC();
+        const double i00 = rsq_nr(pnl[o]);
+        const double l10 = pnl[o + 1] * i00, l20 = pnl[o + 2] * i00;
+        const double i11 = rsq_nr(pnl[16 + o + 1] - l10 * l10);
+        const double l21 = (pnl[16 + o + 2] - l20 * l10) * i11;
+        const double i22 = rsq_nr(pnl[32 + o + 2] - l20 * l20 - l21 * l21);
+        const double z0 = i00 * a[o];
+        const double z1 = (a[o + 1] - l10 * z0) * i11;
+        const double z2 = (a[o + 2] - l20 * z0 - l21 * z1) * i22;
+        const int rest = amask >> (blk + 1);
+        if (blk < 4 && rest) {
+            const double y2 = z2 * i22;
+            const double y1 = (z1 - l21 * y2) * i11;
+            const double y0 = (z0 - l10 * y1 - l20 * y2) * i00;
+            const int nb = blk + 1 + __builtin_ctz(rest);
+#pragma unroll
+            for (int r = o + 3; r < o + 6; ++r) a[r] -= pnl[r] * y0 + pnl[16 + r] * y1 + pnl[32 + r] * y2;
+            const bool pub = lane >= 3 * nb && lane < 3 * nb + 3;
+            ldouble* nx = PNL + (par ^ 1) * 48 + (pub ? (lane - 3 * nb) * 16 : 0);
+            if (pub && nb == blk + 1) {
+#pragma unroll
+                for (int r = o + 3; r < o + 6; ++r) nx[r] = a[r];
+            }
+#pragma unroll
+            for (int r = o + 6; r < 15; ++r) a[r] -= pnl[r] * y0 + pnl[16 + r] * y1 + pnl[32 + r] * y2;
+            if (pub) {
+#pragma unroll
+                for (int r = o + 6; r < 15; ++r) nx[r] = a[r];
+            }
+        }
+        a[o] = z0;
+        a[o + 1] = z1;
+        a[o + 2] = z2;
+        par ^= 1;
+    }
+    // lanes 16+c hold column c of L^-1: stage it (stride 17), then read both tile orientations
+    if (lane >= 16 && lane < 32) {
+        const int c = lane - 16;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) li[c * 17 + r] = a[r];
+    }
+    LMPC_SYNC();
+    DiagInv out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        out.uit[i] = li[lc * 17 + r];  // (r, c) = L^-1[r][c]
+        out.ui[i] = li[r * 17 + lc];   // (r, c) = L^-1[c][r]
+    }
+    return out;
+}
+
+// coupled-block mask of tile t (bits 0-4: leg-steps 5t..5t+4 valid, and with use_act also coupled)
+__device__ __forceinline__ int tile_mask(const DSmem& S, int t, int nls, bool use_act) {
+    int m = 0;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int b = 5 * t + s;
+        if (b < nls && (!use_act || S.act[b < 20 ? b : 0] != 0.0)) m |= 1 << s;
+    }
+    return __builtin_amdgcn_readfirstlane(m);
+}
+
+// lane-wise y = H x for the variables (lane v = variable v), H from its upper tiles in LDS.
+// Lane v walks the columns starting at its own index, so a wave's reads spread over the banks.
+__device__ __forceinline__ double h_matvec(const DSmem& S, const ldouble* x, int NT, int lane) {
+    const int tv = lane >> 4, wv = lane & 15;
+    const int n = 16 * NT;
+    double acc = 0.0;
+    if (tv < NT) {
+        int w = lane;
+        for (int it = 0; it < n; ++it) {
+            w = (w + 1 == n) ? 0 : w + 1;
+            const int tw = w >> 4, ww = w & 15;
+            const int idx = (tv <= tw) ? tix(tv, tw) * DN_TILE + toff(wv, ww) : tix(tw, tv) * DN_TILE + toff(ww, wv);
+            acc = fma(S.Ht[idx], x[w], acc);
+        }
+    }
+    return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Prologue: record -> LDS, stance leg-step map (lsm, fb), terrain frames, I_w^-1, G0 = B rows 6-11,
+// yaw cos/sin of every step, per-leg input Hessian blocks.  smask = ballot of stance leg-steps
+// (lane 4k + j).  Returns this lane's rank among the stance leg-steps (valid when stl).
+// ---------------------------------------------------------------------------
+template <bool TERRAIN>
+__device__ __forceinline__ int dense_prologue(const DevParams& prm, const DSmem& S, const double* __restrict__ rec,
+                                              const double* __restrict__ normals, int qp, int H,
+                                              unsigned long long smask, bool stl, int lane) {
+    const int RL = 33 + 12 * H;
+    const double dt = prm.dt;
+    // ---- record, leg-step map ----
+    const double* rin = rec + (size_t)qp * RL;
+    for (int i = lane; i < RL; i += 64) {
+        const double v = rin[i];
+        if (i < 33) S.hdr[i] = v;
+        else S.xr[i - 33] = v;
+    }
+    const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(smask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)smask, 0));
+    if (stl) S.lsm[rank] = lane;
+    if (lane <= H) {
+        // first stance leg-step of step `lane` = stance leg-steps with 4k + j < 4 lane
+        const unsigned long long below = (lane >= 16) ? smask : (smask & ((1ull << (4 * lane)) - 1ull));
+        S.fb[lane] = __popcll(below);
+    }
+    if (TERRAIN && lane < 4) {
+        const double* nin = normals + (size_t)qp * 12 + 3 * lane;
+        const double n0 = nin[0], n1 = nin[1], n2 = nin[2];
+        const double nn = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+        const double nx = n0 / nn, ny = n1 / nn, c = n2 / nn;
+        const double h = 1.0 / (1.0 + c);
+        const double R[9] = {1.0 - nx * nx * h, -nx * ny * h, nx, -nx * ny * h, 1.0 - ny * ny * h, ny, -nx, -ny, c};
+#pragma unroll
+        for (int e = 0; e < 9; ++e) S.tf[9 * lane + e] = R[e];
+    }
+    LMPC_SYNC();
+    double iw[9];
+    {
+        const ldouble* R = S.hdr + LMPC_REC_ROT;
+        double RI[9], Iw[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                RI[i * 3 + j] = R[i * 3 + 0] * prm.Ib[0 * 3 + j] + R[i * 3 + 1] * prm.Ib[1 * 3 + j] + R[i * 3 + 2] * prm.Ib[2 * 3 + j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                Iw[i * 3 + j] = RI[i * 3 + 0] * R[j * 3 + 0] + RI[i * 3 + 1] * R[j * 3 + 1] + RI[i * 3 + 2] * R[j * 3 + 2];
+        const double c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
+        const double c01 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
+        const double c02 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
+        const double id = 1.0 / (Iw[0] * c00 + Iw[1] * c01 + Iw[2] * c02);
+        iw[0] = c00 * id;
+        iw[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * id;
+        iw[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * id;
+        iw[3] = c01 * id;
+        iw[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * id;
+        iw[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * id;
+        iw[6] = c02 * id;
+        iw[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * id;
+        iw[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * id;
+    }
+    for (int k = lane; k < H; k += 64) {
+        double sn, cn;
+        sincos(S.xr[12 * k + 2], &sn, &cn);
+        S.cs[2 * k] = cn;
+        S.cs[2 * k + 1] = sn;
+    }
+    for (int e = lane; e < 72; e += 64) {
+        const int r = e / 12, c = e % 12, j = c / 3, cc = c % 3;
+        double w[3];
+        if (r < 3) {
+            const ldouble* ft = S.hdr + LMPC_REC_FEET + 3 * j;
+            w[0] = dt * (iw[r * 3 + 1] * ft[2] - iw[r * 3 + 2] * ft[1]);
+            w[1] = dt * (-iw[r * 3 + 0] * ft[2] + iw[r * 3 + 2] * ft[0]);
+            w[2] = dt * (iw[r * 3 + 0] * ft[1] - iw[r * 3 + 1] * ft[0]);
+        } else {
+            w[0] = w[1] = w[2] = 0.0;
+            w[r - 3] = dt / prm.mass;
+        }
+        double v = w[cc];
+        if constexpr (TERRAIN) {
+            const ldouble* Rj = S.tf + 9 * j;
+            v = w[0] * Rj[cc] + w[1] * Rj[3 + cc] + w[2] * Rj[6 + cc];
+        }
+        S.G0[e] = v;
+    }
+    if (lane < 4) {
+        const double r0 = prm.r[3 * lane], r1 = prm.r[3 * lane + 1], r2 = prm.r[3 * lane + 2];
+        if constexpr (TERRAIN) {
+            const ldouble* R = S.tf + 9 * lane;
+            int e = 0;
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = a; b < 3; ++b)
+                    S.rb[6 * lane + e++] = r0 * R[a] * R[b] + r1 * R[3 + a] * R[3 + b] + r2 * R[6 + a] * R[6 + b];
+        } else {
+            S.rb[6 * lane + 0] = r0;
+            S.rb[6 * lane + 1] = 0.0;
+            S.rb[6 * lane + 2] = 0.0;
+            S.rb[6 * lane + 3] = r1;
+            S.rb[6 * lane + 4] = 0.0;
+            S.rb[6 * lane + 5] = r2;
+        }
+    }
+    S.vec[lane] = 0.0;
+    S.vec2[lane] = 0.0;
+    LMPC_SYNC();
+
+    return rank;
+}
+
+}  // namespace lmpc

@@ -22,7 +22,9 @@ struct DevParams {
     int max_iter;      // IPM iteration cap (per attempt)
     int max_rounds;    // polish rounds per attempt
     int max_attempts;  // IPM+polish attempts (tol_mu tightened x1e-3 per attempt)
-    int dense;         // 1: QPs with 1..DENSE_MAX_LS stance leg-steps go to the condensed dense kernel
+    int dense;         // QPs with 1..DENSE_MAX_LS stance leg-steps: 0 Riccati kernel, 1 condensed interior
+                       // point (lmpc_dense.hip), 2 condensed dual active set (lmpc_gi.hip)
+    int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel
 };
 constexpr int DENSE_MAX_LS = 20;  // 5 leg-steps per 16-wide tile x 4 tiles (lmpc_dense.hip)
 constexpr int DENSE_MAX_H = 16;   // the dense path's per-step LDS arrays

@@ -796,16 +796,18 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                                                      const uint8_t* __restrict__ contact,
                                                      const double* __restrict__ normals, int batch,
                                                      double* __restrict__ grf, int32_t* __restrict__ status,
-                                                     int32_t* __restrict__ iters, double* __restrict__ scratch) {
+                                                     int32_t* __restrict__ iters, double* __restrict__ scratch,
+                                                     const uint8_t* __restrict__ dense_done) {
     extern __shared__ __attribute__((aligned(16))) double lmpc_smem[];
     const int qp = blockIdx.x;
     if (qp >= batch) return;
     const int lane = threadIdx.x;
     const int H = prm.H;
-    if (prm.dense) {  // QPs with 1..DENSE_MAX_LS stance leg-steps are solved by lmpc_dense_kernel (H <= 16 here)
+    if (prm.dense) {  // QPs with 1..DENSE_MAX_LS stance leg-steps went to a dense-path kernel (H <= 16 here)
         const bool stl = lane < 4 * H && contact[(size_t)qp * 4 * H + lane] != 0;
         const int n = __popcll(__ballot(stl));
-        if (n >= 1 && n <= DENSE_MAX_LS) return;
+        // the GI kernel flags the QPs it solved; the ones it left (step cap, non-finite step) are solved here
+        if (n >= 1 && n <= DENSE_MAX_LS && (!dense_done || dense_done[qp])) return;
     }
     const int RL = 33 + 12 * H;
     const Smem S = carve(lmpc_smem, H);
@@ -1300,7 +1302,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
 
 #define LMPC_INST(LS_, T_)                                                                                      \
     template __global__ void lmpc_qp_kernel<LS_, T_>(const DevParams, const double*, const uint8_t*, const double*, \
-                                                     int, double*, int32_t*, int32_t*, double*);
+                                                     int, double*, int32_t*, int32_t*, double*, const uint8_t*);
 LMPC_INST(1, false)
 LMPC_INST(2, false)
 LMPC_INST(1, true)
@@ -1310,25 +1312,26 @@ LMPC_INST(2, true)
 template <int LS, bool TERRAIN>
 static void launch_variant(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                            int batch, double* grf, int32_t* status, int32_t* iters, double* scratch,
-                           hipStream_t stream) {
+                           const uint8_t* done, hipStream_t stream) {
     const size_t lds = lds_bytes(prm.H, TERRAIN);
     const dim3 grid(batch), block(LMPC_WAVE);  // LMPC_SYNC() relies on exactly one wavefront per workgroup
     (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<LS, TERRAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     hipLaunchKernelGGL((lmpc_qp_kernel<LS, TERRAIN>), grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
-                       status, iters, scratch);
+                       status, iters, scratch, done);
 }
 
 // Host-side launcher (called from lmpc_capi.cpp).  normals == nullptr: flat ground (the reference).
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
-                     int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, hipStream_t stream) {
+                     int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, const uint8_t* done,
+                     hipStream_t stream) {
     const bool two = 4 * prm.H > 64;
     if (normals) {
-        if (two) launch_variant<2, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
-        else launch_variant<1, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
+        if (two) launch_variant<2, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        else launch_variant<1, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
     } else {
-        if (two) launch_variant<2, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
-        else launch_variant<1, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, stream);
+        if (two) launch_variant<2, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        else launch_variant<1, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
     }
     return hipGetLastError();
 }

@@ -75,11 +75,14 @@ def test_full_config2_batch_vs_oracle():
     assert rel_err(grf, ref) <= TOL_REGRESS
 
 
-@pytest.mark.parametrize("cid", [3, 4, 5])
-def test_full_size_properties(cid, torch_dev):
+@pytest.mark.parametrize("cid,mode", [(3, "ipm"), (4, "ipm"), (4, "gi"), (5, "ipm")])
+def test_full_size_properties(cid, mode, torch_dev, monkeypatch):
     """Configs 3/4/5 at full batch: converged, feasible, swing legs exactly zero,
-    bitwise deterministic, permutation-invariant and shard-invariant."""
+    bitwise deterministic, permutation-invariant and shard-invariant (config 4 also with the
+    dual active-set kernel on its dense-eligible QPs)."""
     import torch
+
+    monkeypatch.setenv("LMPC_DENSE", mode)
 
     p, H, rec, con = synth.config_batch(cid)
     B = rec.shape[0]
@@ -232,10 +235,15 @@ def test_cpp_dropin_program_vs_oracle():
     assert ticks == 3
 
 
-def test_solve_options_and_status_codes():
+@pytest.mark.parametrize("mode", ["ipm", "0"])
+def test_solve_options_and_status_codes(mode, monkeypatch):
+    """IPM options (max_iter / attempts) on the two interior-point paths: the condensed dense kernel
+    (LMPC_DENSE=ipm) and the Riccati kernel (LMPC_DENSE=0).  The dual active-set kernel has no
+    interior-point iterations; its step cap hands a QP to the Riccati kernel."""
     from legged_mpc_control_amd import LmpcOptions
     from legged_mpc_control_amd import _native as N
 
+    monkeypatch.setenv("LMPC_DENSE", mode)
     p, H, rec, con = synth.config_batch(2, count=32)
     s = BatchedConvexQPSolver(p, H, max_batch=32)
     o = LmpcOptions()
@@ -336,15 +344,18 @@ def test_terrain_rejects_bad_normals():
 # ---------------------------------------------------------------------------
 # the two device paths: condensed dense kernel (<= 20 stance leg-steps, H <= 16) and Riccati kernel
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["ipm", "gi"])
 @pytest.mark.parametrize("cid", [2, 4])
-def test_dense_and_riccati_paths_agree(cid, monkeypatch):
-    """Every config-2 QP (and the trot-like config-4 QPs) runs on the dense path by default; with
-    LMPC_DENSE=0 the same QPs run on the Riccati path.  Both must give the oracle's optimum."""
+def test_dense_and_riccati_paths_agree(cid, mode, monkeypatch):
+    """Every config-2 QP (and the trot-like config-4 QPs) runs on a condensed dense kernel -- the
+    interior point (LMPC_DENSE=ipm) or the dual active set (LMPC_DENSE=gi); with LMPC_DENSE=0 the
+    same QPs run on the Riccati path.  All must give the oracle's optimum."""
     p, H, rec, con = synth.config_batch(cid, count=512, first_index=777)
     nrm = synth.config_normals(cid, count=512, first_index=777)
     nls = con.sum((1, 2))
-    assert np.any(nls <= 20) and (cid == 4 or np.all(nls <= 20))
-    monkeypatch.setenv("LMPC_DENSE", "1")
+    dense = (nls >= 1) & (nls <= 20)
+    assert np.any(dense) and (cid == 4 or np.all(dense))
+    monkeypatch.setenv("LMPC_DENSE", mode)
     gd, sd, itd = BatchedConvexQPSolver(p, H, max_batch=512).solve(rec, con, normals=nrm)
     monkeypatch.setenv("LMPC_DENSE", "0")
     gr, sr, itr = BatchedConvexQPSolver(p, H, max_batch=512).solve(rec, con, normals=nrm)
@@ -352,14 +363,22 @@ def test_dense_and_riccati_paths_agree(cid, monkeypatch):
     assert fails == 0 and np.all(sd == 0) and np.all(sr == 0)
     assert rel_err(gd, ref) <= TOL_REGRESS and rel_err(gr, ref) <= TOL_REGRESS
     assert rel_err(gd, gr) <= 1e-8
-    # same Newton systems, so the same iteration counts on both paths
-    assert np.mean(np.abs((itd & 0xFFFF) - (itr & 0xFFFF))) < 0.05
+    if mode == "ipm":
+        # same Newton systems, so the same iteration counts on both paths
+        assert np.mean(np.abs((itd & 0xFFFF) - (itr & 0xFFFF))) < 0.05
+    else:
+        # dual active set: steps in the low 16 bits (0 when the unconstrained minimiser is feasible),
+        # drops in the high bits
+        steps, drops = itd[dense] & 0xFFFF, itd[dense] >> 16
+        assert np.all(drops <= steps) and steps.mean() > 5
+        assert np.array_equal(itd[~dense], itr[~dense])  # the rest ran on the Riccati kernel
 
 
-def test_dense_path_edge_cases(monkeypatch):
+@pytest.mark.parametrize("mode", ["ipm", "gi"])
+def test_dense_path_edge_cases(mode, monkeypatch):
     """Dense-path QPs with fewer than 20 stance leg-steps (partly padded tiles), a single stance
     leg-step, and the all-swing QP (left to the Riccati kernel)."""
-    monkeypatch.setenv("LMPC_DENSE", "1")
+    monkeypatch.setenv("LMPC_DENSE", mode)
     p, H, rec, con = synth.config_batch(2, count=8, first_index=31)
     con = con.copy()
     con[0, :, :] = 0; con[0, 0, 1] = 1          # one stance leg-step
@@ -373,3 +392,22 @@ def test_dense_path_edge_cases(monkeypatch):
     assert fails == 0 and np.all(st == 0), st
     assert rel_err(g, ref) <= TOL_REGRESS
     assert np.all(g[2] == 0.0)
+
+
+def test_gi_step_cap_hands_over_to_riccati(monkeypatch):
+    """A dual active-set QP that reaches the step cap is solved by the Riccati kernel in the same
+    launch: same optimum, and its iteration word carries the interior-point counts (polish rounds
+    >= 1 in the high bits) instead of the active-set steps."""
+    p, H, rec, con = synth.config_batch(2, count=256, first_index=4242)
+    monkeypatch.setenv("LMPC_DENSE", "gi")
+    monkeypatch.setenv("LMPC_GI_MAX_STEPS", "20")
+    g, st, it = BatchedConvexQPSolver(p, H, max_batch=256).solve(rec, con)
+    monkeypatch.setenv("LMPC_GI_MAX_STEPS", "1000")
+    g2, st2, it2 = BatchedConvexQPSolver(p, H, max_batch=256).solve(rec, con)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
+    assert fails == 0 and np.all(st == 0) and np.all(st2 == 0)
+    handed = (it2 & 0xFFFF) > 20
+    assert 0 < handed.sum() < 256
+    assert np.all((it[handed] >> 16) >= 1)        # Riccati: polish rounds in the high bits
+    assert np.array_equal(it[~handed], it2[~handed])
+    assert rel_err(g, ref) <= TOL_REGRESS and rel_err(g2, ref) <= TOL_REGRESS

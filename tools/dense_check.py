@@ -15,8 +15,11 @@ from legged_mpc_control_amd import BatchedConvexQPSolver, synth  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
-def solver(p, H, B, dense):
-    os.environ["LMPC_DENSE"] = "1" if dense else "0"
+MODES = {"gi": "gi", "ipm": "ipm", "riccati": "0"}
+
+
+def solver(p, H, B, mode):
+    os.environ["LMPC_DENSE"] = MODES[mode]
     return BatchedConvexQPSolver(p, H, B)
 
 
@@ -25,7 +28,7 @@ def main():
         p, H, rec, con = synth.config_batch(cid, count=cnt)
         nrm = synth.config_normals(cid, count=cnt)
         ref, _, _ = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8, normals=nrm)
-        for dense in (True, False):
+        for dense in ("gi", "ipm", "riccati"):
             g, st, it = solver(p, H, cnt, dense).solve(rec, con, normals=nrm)
             err = np.max(np.abs(g - ref) / np.maximum(1.0, np.abs(ref)))
             nls = (con.sum((1, 2)))
@@ -39,7 +42,7 @@ def main():
     # timing, config 2 full batch
     p, H, rec, con = synth.config_batch(2)
     dev = torch.device("cuda", 0)
-    for dense in (True, False, True):
+    for dense in ("gi", "ipm", "riccati", "gi"):
         s = solver(p, H, len(rec), dense)
         d = [torch.from_numpy(rec).to(dev), torch.from_numpy(con).to(dev),
              torch.empty((len(rec), H, 12), dtype=torch.float64, device=dev),
@@ -65,7 +68,7 @@ def stamps():
 
     from legged_mpc_control_amd import _native as N
     p, H, rec, con = synth.config_batch(2)
-    s = solver(p, H, len(rec), True)
+    s = solver(p, H, len(rec), "ipm")
     g, st, it = s.solve(rec, con)
     L = N.lib()
     L.lmpc_debug_dense_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -79,10 +82,38 @@ def stamps():
         print(f"  {nm:20s} {v:10.0f} ({100 * v / tot.mean():5.1f}%)")
 
 
+def gi_stamps():
+    """Per-phase cycles of the GI kernel (needs the -DLMPC_STAMPS library)."""
+    import ctypes
+
+    from legged_mpc_control_amd import _native as N
+    p, H, rec, con = synth.config_batch(2)
+    s = solver(p, H, len(rec), "gi")
+    g, st, it = s.solve(rec, con)
+    L = N.lib()
+    L.lmpc_debug_gi_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = np.zeros((1024, 8), dtype=np.uint64)
+    n = L.lmpc_debug_gi_stamps(buf.ctypes.data, 1024)
+    names = ["prologue+condense", "cholesky+x0+J", "violation search", "d = J'n", "z, r", "step+add",
+             "step+drop", "output"]
+    tot = buf[:n, :8].sum(1).astype(float)
+    steps = it[:n] & 0xffff
+    print(f"gi config 2: mean cycles/QP {tot.mean():.0f} max {tot.max():.0f} (steps mean {steps.mean():.1f} max {steps.max()})")
+    for i, nm in enumerate(names):
+        v = buf[:n, i].astype(float)
+        print(f"  {nm:20s} mean {v.mean():10.0f} ({100 * v.mean() / tot.mean():5.1f}%) max {v.max():10.0f}")
+    w = int(np.argmax(tot))
+    print(f"  slowest QP {w}: {tot[w]:.0f} cycles, {steps[w]} steps, {it[w] >> 16} drops: " +
+          ", ".join(f"{nm} {buf[w, i]}" for i, nm in enumerate(names)))
+    per = buf[:n, 2:7].sum(1).astype(float) / np.maximum(steps, 1)
+    print(f"  cycles per active-set step: mean {per.mean():.0f}")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "stamps":
         from legged_mpc_control_amd import build as B
         os.environ["LMPC_LIB"] = B.build_stamps()
         stamps()
+        gi_stamps()
     else:
         main()
