@@ -41,6 +41,17 @@ def parse():
     return ap.parse_args()
 
 
+def kernel_label(H):
+    """The kernels of one solve launch (lmpc_capi.cpp lmpc_solve_batch_device_ex); kernel_ms covers all."""
+    from legged_mpc_control_amd.solver import dense_mode
+
+    mode = dense_mode(H)
+    if mode == "riccati":
+        return "lmpc_qp_kernel (Riccati, every QP)"
+    dense = "lmpc_gi_kernel" if mode == "gi" else "lmpc_dense_kernel"
+    return f"{dense} (QPs with <= 20 stance leg-steps) + lmpc_qp_kernel (the rest; exits at once when none)"
+
+
 def global_batch_of(strong, cfg, B, world):
     return cfg["batch"] if strong else B * world
 
@@ -143,9 +154,17 @@ def main():
     grf = d_grf.cpu().numpy()
     st = d_st.cpu().numpy()
     it = d_it.cpu().numpy()
+    from legged_mpc_control_amd.solver import dense_mode
+
+    mode = dense_mode(H)
     ipm_mean = float(np.mean(it & 0xFFFF))
     pol_mean = float(np.mean(it >> 16))
-    flop_per_qp = roofline.survey_flop(H, ipm_mean, pol_mean)  # SURVEY.md 8(d) contract figure
+    if mode == "gi":  # iteration word = active-set steps | drops << 16 on the dense QPs
+        flop_per_qp = roofline.gi_flop(H, ipm_mean)
+        flop_model = "SURVEY.md 8(d) F0 + steps * 6 * 64^2 (dual active set; steps = measured mean)"
+    else:
+        flop_per_qp = roofline.survey_flop(H, ipm_mean, pol_mean)  # SURVEY.md 8(d) contract figure
+        flop_model = "SURVEY.md 8(d): F0 + K*F_iter + rounds*(N^3/3 + 2N^2), K/rounds = measured means"
     riccati_flop_per_qp = roofline.qp_flop(H, ipm_mean, pol_mean)  # the build's own useful-flop count
     achieved_tf = flop_per_qp * B / (kernel_ms * 1e-3) / 1e12
     global_batch = global_batch_of(strong, cfg, B, world)
@@ -222,10 +241,10 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / roofline.FP64_PEAK_TFLOPS,
                 "traffic": traffic_bytes,
-                "kernel": "lmpc_qp_kernel",
+                "kernel": kernel_label(H),
                 "kernel_ms": kernel_ms,
                 "flop_per_qp": flop_per_qp,
-                "flop_model": "SURVEY.md 8(d): F0 + K*F_iter + rounds*(N^3/3 + 2N^2), K/rounds = measured means",
+                "flop_model": flop_model,
                 "riccati_flop_per_qp": riccati_flop_per_qp,
                 "hbm_gbs": roofline.qp_bytes(H) * B / (kernel_ms * 1e-3) / 1e9,
             },
@@ -233,6 +252,7 @@ def main():
             "with_gather": with_gather,
             "max_grf_err": max_err,
             "qp_status": {"converged": int(stats[0]), "max_iter": int(stats[1]), "nan": int(stats[2])},
+            "dense_path": mode,
             "ipm_iters_mean": ipm_mean,
             "polish_rounds_mean": pol_mean,
             "ipm_iters_max": int(np.max(it & 0xFFFF)),

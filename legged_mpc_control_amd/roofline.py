@@ -70,6 +70,13 @@ def survey_flop(H: int, iters: float, polish_rounds: float) -> float:
     return survey_f0(H) + iters * survey_f_iter(H) + polish_rounds * (N ** 3 / 3 + 2 * N * N)
 
 
+def gi_flop(H: int, steps: float) -> float:
+    """Dual active-set path (lmpc_gi.hip): SURVEY.md 8(d)'s F0 (condensation + one factorisation) plus,
+    per active-set step, z = J2 d2 (2 N^2) and the Householder update of J (4 N^2) on the padded
+    N = 64 dense dimension (the R^-1 product and the 3-row d = J'n are lower order)."""
+    return survey_f0(H) + steps * 6 * 64 * 64
+
+
 def qp_bytes(H: int) -> int:
     """HBM bytes per QP: record (33+12H doubles) + contact (4H) + GRF out (12H doubles) + status + iters."""
     return (33 + 12 * H) * 8 + 4 * H + 12 * H * 8 + 8

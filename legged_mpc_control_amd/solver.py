@@ -25,6 +25,20 @@ def _dp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
+DENSE_MAX_H = 16  # lmpc_device.h: horizons with a condensed dense path
+
+
+def dense_mode(H: int) -> str:
+    """Which kernel a context created now solves the QPs with <= 20 stance leg-steps on
+    (lmpc_create reads LMPC_DENSE): "ipm" (default), "gi" or "riccati"."""
+    import os
+
+    v = os.environ.get("LMPC_DENSE", "")
+    if H > DENSE_MAX_H or v.startswith("0"):
+        return "riccati"
+    return "gi" if v.startswith("g") else "ipm"
+
+
 def leg_kin_default() -> N.LmpcLegKin:
     """The reference's leg constants (BaseInterface.cpp:76-97)."""
     k = N.LmpcLegKin()
