@@ -42,8 +42,13 @@ def torch_dev():
     return torch.device("cuda:0")
 
 
+@pytest.mark.parametrize("mode", ["ipm", "gi", "0"])
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: os.path.basename(p))
-def test_golden_fixtures(path):
+def test_golden_fixtures(path, mode, monkeypatch):
+    """Every certified golden instance on each device path: the condensed interior point (default),
+    the condensed dual active set and the Riccati kernel (QPs the dense kernels do not take -- more
+    than 20 stance leg-steps, H > 16, all-swing -- run on the Riccati kernel in every mode)."""
+    monkeypatch.setenv("LMPC_DENSE", mode)
     g = load_golden(path)
     s = BatchedConvexQPSolver(lmpc_params_from(g["params"]), g["H"], max_batch=g["rec"].shape[0])
     grf, status, iters = s.solve(g["rec"], g["contact"], normals=g["normals"])
