@@ -485,38 +485,9 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                         changed = 1;
                     }
                 } else if (act != 0) {
-                    int idx[3], nr = 0;
-                    for (int i = 0; i < 5 && nr < 3; ++i)
-                        if ((act >> i) & 1) idx[nr++] = i;
-                    double Cs[3][3], Gm[3][3], rhs[3];
-                    for (int a = 0; a < nr; ++a) {
-                        cons_rowvec(idx[a], mu, Cs[a]);
-                        rhs[a] = -(Cs[a][0] * g[0] + Cs[a][1] * g[1] + Cs[a][2] * g[2]);
-                    }
-                    for (int a = 0; a < nr; ++a)
-                        for (int b2 = 0; b2 < nr; ++b2)
-                            Gm[a][b2] = Cs[a][0] * Cs[b2][0] + Cs[a][1] * Cs[b2][1] + Cs[a][2] * Cs[b2][2];
-                    for (int a = 0; a < nr; ++a)
-                        for (int b2 = a + 1; b2 < nr; ++b2) {
-                            const double fct = Gm[b2][a] / Gm[a][a];
-                            for (int c2 = a; c2 < nr; ++c2) Gm[b2][c2] -= fct * Gm[a][c2];
-                            rhs[b2] -= fct * rhs[a];
-                        }
-                    double zz[3];
-                    for (int a = nr - 1; a >= 0; --a) {
-                        double v = rhs[a];
-                        for (int b2 = a + 1; b2 < nr; ++b2) v -= Gm[a][b2] * zz[b2];
-                        zz[a] = v / Gm[a][a];
-                    }
-                    int amin = -1;
-                    double zmin = -prm.tol_d * gscale;
-                    for (int a = 0; a < nr; ++a)
-                        if (zz[a] < zmin) {
-                            zmin = zz[a];
-                            amin = a;
-                        }
-                    if (amin >= 0) {
-                        act &= ~(1 << idx[amin]);
+                    const int df = leg_drop_face(act, g, mu, -prm.tol_d * gscale);
+                    if (df >= 0) {
+                        act &= ~(1 << df);
                         changed = 1;
                     }
                 }

@@ -115,51 +115,92 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
 
+// Up to three active faces of a leg-step, in face order (slot k: face index, 7 = unused slot).
+// Everything below is statically indexed over 3 slots (a dynamically indexed per-lane array is
+// placed in scratch memory: 30+ scratch round trips per polish round in both QP kernels).
+struct ActiveRows {
+    int i0, i1, i2, nr;
+};
+__device__ __forceinline__ ActiveRows active_rows(int act) {
+    ActiveRows r;
+    int m = act & 31;
+    r.i0 = m ? __builtin_ctz(m) : 7;
+    m &= m - 1;
+    r.i1 = m ? __builtin_ctz(m) : 7;
+    m &= m - 1;
+    r.i2 = m ? __builtin_ctz(m) : 7;
+    r.nr = (r.i0 < 5) + (r.i1 < 5) + (r.i2 < 5);
+    return r;
+}
+
 // Null-space parametrisation of one leg-step for active set `act` (bit i = row ci):
 // f = up + T y, T columns orthonormal.  Returns true at the pyramid apex (f = 0).
-__device__ bool leg_basis(int act, double mu, double fzmax, double T[9], double up[3]) {
+__device__ __forceinline__ bool leg_basis(int act, double mu, double fzmax, double T[9], double up[3]) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) T[i] = 0.0;
     up[0] = up[1] = up[2] = 0.0;
     if ((act & 3) == 3 || (act & 12) == 12) return true;
-    double rows[3][3], bs[3];
-    int nr = 0;
-    for (int i = 0; i < 5; ++i) {
-        if (!((act >> i) & 1) || nr >= 3) continue;
-        cons_rowvec(i, mu, rows[nr]);
-        bs[nr] = (i == 4) ? fzmax : 0.0;
-        ++nr;
-    }
-    double qv[3][3];
-    for (int a = 0; a < nr; ++a) {
-        double v[3] = {rows[a][0], rows[a][1], rows[a][2]};
-        for (int b = 0; b < a; ++b) {
-            const double d = qv[b][0] * v[0] + qv[b][1] * v[1] + qv[b][2] * v[2];
-            v[0] -= d * qv[b][0];
-            v[1] -= d * qv[b][1];
-            v[2] -= d * qv[b][2];
-        }
-        const double n = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-        qv[a][0] = v[0] * n;
-        qv[a][1] = v[1] * n;
-        qv[a][2] = v[2] * n;
+    const ActiveRows ar = active_rows(act);
+    const int nr = ar.nr;
+    double r0[3], r1[3], r2[3];
+    cons_rowvec(ar.i0, mu, r0);
+    cons_rowvec(ar.i1, mu, r1);
+    cons_rowvec(ar.i2, mu, r2);
+    const double b0 = ar.i0 == 4 ? fzmax : 0.0, b1 = ar.i1 == 4 ? fzmax : 0.0, b2 = ar.i2 == 4 ? fzmax : 0.0;
+    // Gram-Schmidt (slots beyond nr are computed on dummy rows and never used)
+    double q0[3], q1[3], q2[3];
+    {
+        const double n = 1.0 / sqrt(r0[0] * r0[0] + r0[1] * r0[1] + r0[2] * r0[2]);
+        q0[0] = r0[0] * n;
+        q0[1] = r0[1] * n;
+        q0[2] = r0[2] * n;
     }
     {
-        double beta[3] = {0.0, 0.0, 0.0};
-        for (int a = 0; a < nr; ++a) {
-            double s = bs[a];
-            for (int b = 0; b < a; ++b)
-                s -= (rows[a][0] * qv[b][0] + rows[a][1] * qv[b][1] + rows[a][2] * qv[b][2]) * beta[b];
-            const double diag = rows[a][0] * qv[a][0] + rows[a][1] * qv[a][1] + rows[a][2] * qv[a][2];
-            beta[a] = s / diag;
+        double v[3] = {r1[0], r1[1], r1[2]};
+        const double d = q0[0] * v[0] + q0[1] * v[1] + q0[2] * v[2];
+        v[0] -= d * q0[0];
+        v[1] -= d * q0[1];
+        v[2] -= d * q0[2];
+        const double n = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        q1[0] = v[0] * n;
+        q1[1] = v[1] * n;
+        q1[2] = v[2] * n;
+    }
+    {
+        double v[3] = {r2[0], r2[1], r2[2]};
+        double d = q0[0] * v[0] + q0[1] * v[1] + q0[2] * v[2];
+        v[0] -= d * q0[0];
+        v[1] -= d * q0[1];
+        v[2] -= d * q0[2];
+        d = q1[0] * v[0] + q1[1] * v[1] + q1[2] * v[2];
+        v[0] -= d * q1[0];
+        v[1] -= d * q1[1];
+        v[2] -= d * q1[2];
+        const double n = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        q2[0] = v[0] * n;
+        q2[1] = v[1] * n;
+        q2[2] = v[2] * n;
+    }
+    // particular solution up = sum_a beta_a q_a with rows_a . up = b_a
+    if (nr >= 1) {
+        const double beta0 = b0 / (r0[0] * q0[0] + r0[1] * q0[1] + r0[2] * q0[2]);
+        double beta1 = 0.0, beta2 = 0.0;
+        if (nr >= 2) {
+            const double s1 = b1 - (r1[0] * q0[0] + r1[1] * q0[1] + r1[2] * q0[2]) * beta0;
+            beta1 = s1 / (r1[0] * q1[0] + r1[1] * q1[1] + r1[2] * q1[2]);
         }
-        for (int a = 0; a < nr; ++a)
-            for (int i = 0; i < 3; ++i) up[i] += beta[a] * qv[a][i];
+        if (nr >= 3) {
+            const double s2 = b2 - (r2[0] * q0[0] + r2[1] * q0[1] + r2[2] * q0[2]) * beta0 -
+                              (r2[0] * q1[0] + r2[1] * q1[1] + r2[2] * q1[2]) * beta1;
+            beta2 = s2 / (r2[0] * q2[0] + r2[1] * q2[1] + r2[2] * q2[2]);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) up[i] = beta0 * q0[i] + (nr >= 2 ? beta1 * q1[i] : 0.0) + (nr >= 3 ? beta2 * q2[i] : 0.0);
     }
     if (nr == 0) {
         T[0] = T[4] = T[8] = 1.0;
     } else if (nr == 1) {
-        const double* n = qv[0];
+        const double* n = q0;
         double e[3] = {0.0, 0.0, 0.0};
         if (fabs(n[0]) < 0.9) e[0] = 1.0;
         else e[1] = 1.0;
@@ -170,17 +211,69 @@ __device__ bool leg_basis(int act, double mu, double fzmax, double T[9], double 
         t1[1] *= in;
         t1[2] *= in;
         const double t2[3] = {n[1] * t1[2] - n[2] * t1[1], n[2] * t1[0] - n[0] * t1[2], n[0] * t1[1] - n[1] * t1[0]};
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
             T[i * 3 + 0] = t1[i];
             T[i * 3 + 1] = t2[i];
         }
     } else if (nr == 2) {
-        double t[3] = {qv[0][1] * qv[1][2] - qv[0][2] * qv[1][1], qv[0][2] * qv[1][0] - qv[0][0] * qv[1][2],
-                       qv[0][0] * qv[1][1] - qv[0][1] * qv[1][0]};
+        double t[3] = {q0[1] * q1[2] - q0[2] * q1[1], q0[2] * q1[0] - q0[0] * q1[2], q0[0] * q1[1] - q0[1] * q1[0]};
         const double in = 1.0 / sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+#pragma unroll
         for (int i = 0; i < 3; ++i) T[i * 3 + 0] = t[i] * in;
     }
     return false;
+}
+
+// Polish verification of one (non-apex) leg-step: multipliers of its active faces from
+// C_S' z = -g (C_S = the <= 3 active rows, full row rank), by Gaussian elimination on the Gram
+// matrix C_S C_S' padded to 3x3 with identity rows.  Returns the face whose multiplier is the most
+// negative below zmin (the one to drop), or -1.
+__device__ __forceinline__ int leg_drop_face(int act, const double g[3], double mu, double zmin) {
+    const ActiveRows ar = active_rows(act);
+    const int nr = ar.nr;
+    double C[3][3];
+    cons_rowvec(ar.i0, mu, C[0]);
+    cons_rowvec(ar.i1, mu, C[1]);
+    cons_rowvec(ar.i2, mu, C[2]);
+    double Gm[3][3], rhs[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        rhs[a] = a < nr ? -(C[a][0] * g[0] + C[a][1] * g[1] + C[a][2] * g[2]) : 0.0;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const double v = C[a][0] * C[b][0] + C[a][1] * C[b][1] + C[a][2] * C[b][2];
+            Gm[a][b] = (a < nr && b < nr) ? v : (a == b ? 1.0 : 0.0);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int b = a + 1; b < 3; ++b) {
+            const double fct = Gm[b][a] / Gm[a][a];
+#pragma unroll
+            for (int c = a; c < 3; ++c) Gm[b][c] -= fct * Gm[a][c];
+            rhs[b] -= fct * rhs[a];
+        }
+    }
+    double zz[3];
+#pragma unroll
+    for (int a = 2; a >= 0; --a) {
+        double v = rhs[a];
+#pragma unroll
+        for (int b = a + 1; b < 3; ++b) v -= Gm[a][b] * zz[b];
+        zz[a] = v / Gm[a][a];
+    }
+    int face = -1;
+    double zm = zmin;
+    const int fi[3] = {ar.i0, ar.i1, ar.i2};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        if (a < nr && zz[a] < zm) {
+            zm = zz[a];
+            face = fi[a];
+        }
+    return face;
 }
 
 }  // namespace lmpc
