@@ -41,12 +41,9 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_label(H):
+def kernel_label(mode):
     """The kernels of one solve launch (lmpc_capi.cpp lmpc_solve_batch_device_ex); kernel_ms covers all."""
-    from legged_mpc_control_amd.solver import dense_mode
-
-    mode = dense_mode(H)
-    if mode == "riccati":
+    if mode == "off":
         return "lmpc_qp_kernel (Riccati, every QP)"
     dense = "lmpc_gi_kernel" if mode == "gi" else "lmpc_dense_kernel"
     return f"{dense} (QPs with <= 20 stance leg-steps) + lmpc_qp_kernel (the rest; exits at once when none)"
@@ -154,9 +151,7 @@ def main():
     grf = d_grf.cpu().numpy()
     st = d_st.cpu().numpy()
     it = d_it.cpu().numpy()
-    from legged_mpc_control_amd.solver import dense_mode
-
-    mode = dense_mode(H)
+    mode = solver.dense_path  # "ipm" (default), "gi" or "off" (H > 16, or LMPC_DENSE=0)
     ipm_mean = float(np.mean(it & 0xFFFF))
     pol_mean = float(np.mean(it >> 16))
     if mode == "gi":  # iteration word = active-set steps | drops << 16 on the dense QPs
@@ -241,7 +236,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / roofline.FP64_PEAK_TFLOPS,
                 "traffic": traffic_bytes,
-                "kernel": kernel_label(H),
+                "kernel": kernel_label(mode),
                 "kernel_ms": kernel_ms,
                 "flop_per_qp": flop_per_qp,
                 "flop_model": flop_model,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LMPC_ABI_VERSION 2 /* 2: terrain-normal extension (_ex entry points) */
+#define LMPC_ABI_VERSION 3 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection */
 #define LMPC_MAX_HORIZON 32
 
 /* return codes (API level) */
@@ -109,6 +109,19 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
 void lmpc_destroy(lmpc_ctx* ctx);
 int lmpc_set_options(lmpc_ctx* ctx, const lmpc_options* o);
 int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
+
+/* Dense path (ABI 3).  QPs with 1..20 stance leg-steps at H <= 16 are solved on the condensed QP by
+ * LMPC_DENSE_IPM (interior point + active-set polish; the default: fastest when every SIMD holds one QP
+ * and the launch waits for its slowest, e.g. 1024 QPs) or LMPC_DENSE_GI (dual active set: about half
+ * the mean cost per QP, a longer tail -- the choice for one QP per call, e.g. the per-tick drop-in);
+ * LMPC_DENSE_OFF sends every QP to the Riccati kernel.  All return the same optimum.  Set it before
+ * solving; the environment variable LMPC_DENSE (0 / ipm / gi), when set, overrides this call.
+ * lmpc_get_dense_path returns the path in effect (LMPC_DENSE_OFF when H > 16). */
+#define LMPC_DENSE_OFF 0
+#define LMPC_DENSE_IPM 1
+#define LMPC_DENSE_GI 2
+int lmpc_set_dense_path(lmpc_ctx* ctx, int path);
+int lmpc_get_dense_path(const lmpc_ctx* ctx);
 
 /* Pre-allocates the per-QP factor workspace for batches up to `batch` (the
  * device path grows it on demand; call this before capturing a HIP graph). */

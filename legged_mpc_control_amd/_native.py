@@ -33,8 +33,10 @@ EXPORTED_SYMBOLS = (
     "lmpc_synth_commands", "lmpc_synth_commands_device", "lmpc_synth_normals_device",
     # GRF -> joint torque
     "lmpc_leg_kin_default", "lmpc_foot_jacobian", "lmpc_grf_to_torque", "lmpc_grf_to_torque_device",
+    # ABI 3: dense-path selection
+    "lmpc_set_dense_path", "lmpc_get_dense_path",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class LmpcParams(ctypes.Structure):
@@ -143,6 +145,10 @@ def lib():
         L.lmpc_set_options.restype = ctypes.c_int
         L.lmpc_set_params.argtypes = [vp, pp]
         L.lmpc_set_params.restype = ctypes.c_int
+        L.lmpc_set_dense_path.argtypes = [vp, ctypes.c_int]
+        L.lmpc_set_dense_path.restype = ctypes.c_int
+        L.lmpc_get_dense_path.argtypes = [vp]
+        L.lmpc_get_dense_path.restype = ctypes.c_int
         L.lmpc_reserve.argtypes = [vp, ctypes.c_int]
         L.lmpc_reserve.restype = ctypes.c_int
         L.lmpc_solve_batch.argtypes = [vp, dp, u8p, ctypes.c_int, dp, i32p, i32p]

@@ -86,5 +86,18 @@ def build_cpp_test(force: bool = False) -> str:
     return out
 
 
+def build_tool_cpp(name: str, force: bool = False) -> str:
+    """Dev tool program over liblmpc.so (tools/<name>.cpp -> tools/build/<name>); never shipped."""
+    src = os.path.join(ROOT, "tools", f"{name}.cpp")
+    out = os.path.join(ROOT, "tools", "build", name)
+    if not force and not _stale(out, [src, LIB]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", out, src,
+           "-L", LIBDIR, "-llmpc", f"-Wl,-rpath,{LIBDIR}"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 if __name__ == "__main__":
     print(build_native(force=True, verbose=True))

@@ -21,6 +21,8 @@ ConvexQPSolver::ConvexQPSolver(const double* q_weights, const double* r_weights,
     contact_.assign((size_t)4 * H_, 1);
     grf_.assign((size_t)12 * H_, 0.0);
     error_ = lmpc_create(&params_, H_, 1, device, &ctx_);
+    // one QP per call: the dual active set has the lower latency (no batch tail to wait for)
+    if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_GI);
 }
 
 ConvexQPSolver::~ConvexQPSolver() { lmpc_destroy(ctx_); }

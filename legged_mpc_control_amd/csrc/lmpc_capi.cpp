@@ -46,6 +46,7 @@ struct lmpc_ctx {
     int32_t* d_iters = nullptr;
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
     uint8_t* d_done = nullptr;    // per-QP flag: solved by the GI kernel (else the Riccati kernel solves it)
+    bool dense_env = false;       // LMPC_DENSE set: it overrides lmpc_set_dense_path
     size_t scratch_qps = 0;
     double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
     uint8_t* d_ccon = nullptr;
@@ -134,6 +135,7 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     // QP (A/B checks).  The choice is fixed per context, never per launch, so a QP's answer does not
     // depend on the batch it is solved in.  Why the interior point is the default: DESIGN.md 4b.
     const char* dn = std::getenv("LMPC_DENSE");
+    c->dense_env = dn && dn[0];
     c->prm.dense = horizon > lmpc::DENSE_MAX_H || (dn && dn[0] == '0') ? 0 : (dn && dn[0] == 'g') ? 2 : 1;
     {
         const char* gm = std::getenv("LMPC_GI_MAX_STEPS");  // test hook: exercise the hand-over to the Riccati kernel
@@ -190,6 +192,14 @@ int lmpc_set_params(lmpc_ctx* c, const lmpc_params* p) {
     fill_params(c->prm, p);
     return LMPC_OK;
 }
+
+int lmpc_set_dense_path(lmpc_ctx* c, int path) {
+    if (!c || path < LMPC_DENSE_OFF || path > LMPC_DENSE_GI) return LMPC_ERR_ARG;
+    if (!c->dense_env && c->H <= lmpc::DENSE_MAX_H) c->prm.dense = path;
+    return LMPC_OK;
+}
+
+int lmpc_get_dense_path(const lmpc_ctx* c) { return c ? c->prm.dense : LMPC_ERR_ARG; }
 
 int lmpc_reserve(lmpc_ctx* c, int batch) {
     if (!c || batch < 0) return LMPC_ERR_ARG;

@@ -25,20 +25,6 @@ def _dp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
-DENSE_MAX_H = 16  # lmpc_device.h: horizons with a condensed dense path
-
-
-def dense_mode(H: int) -> str:
-    """Which kernel a context created now solves the QPs with <= 20 stance leg-steps on
-    (lmpc_create reads LMPC_DENSE): "ipm" (default), "gi" or "riccati"."""
-    import os
-
-    v = os.environ.get("LMPC_DENSE", "")
-    if H > DENSE_MAX_H or v.startswith("0"):
-        return "riccati"
-    return "gi" if v.startswith("g") else "ipm"
-
-
 def leg_kin_default() -> N.LmpcLegKin:
     """The reference's leg constants (BaseInterface.cpp:76-97)."""
     k = N.LmpcLegKin()
@@ -66,8 +52,11 @@ def grf_to_torque(kin: N.LmpcLegKin, rot, joint_pos, grf0) -> np.ndarray:
 class BatchedConvexQPSolver:
     """A device context: horizon H, host staging for up to max_batch QPs."""
 
+    DENSE_PATHS = {"off": 0, "ipm": 1, "gi": 2}
+
     def __init__(self, params: N.LmpcParams, horizon: int, max_batch: int = 1, device: int = 0,
-                 options: N.LmpcOptions | None = None):
+                 options: N.LmpcOptions | None = None, dense_path: str | None = None):
+        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path; LMPC_DENSE overrides it)."""
         if not (1 <= horizon <= N.LMPC_MAX_HORIZON):
             raise ValueError(f"horizon must be in [1, {N.LMPC_MAX_HORIZON}]")
         self._L = N.lib()
@@ -79,6 +68,17 @@ class BatchedConvexQPSolver:
                                     ctypes.byref(self._ctx)), "lmpc_create")
         if options is not None:
             self.set_options(options)
+        if dense_path is not None:
+            self.set_dense_path(dense_path)
+
+    def set_dense_path(self, path: str) -> None:
+        N.check(self._L.lmpc_set_dense_path(self._ctx, self.DENSE_PATHS[path]), "lmpc_set_dense_path")
+
+    @property
+    def dense_path(self) -> str:
+        """The dense-path kernel in effect for this context."""
+        v = self._L.lmpc_get_dense_path(self._ctx)
+        return {0: "off", 1: "ipm", 2: "gi"}[v]
 
     @property
     def record_len(self) -> int:
@@ -320,7 +320,8 @@ class ConvexQPSolver:
         p.mu, p.f_max, p.gravity, p.dt = float(mu), float(f_max), float(gravity), float(dt)
         self.H = int(horizon)
         self._p = p
-        self._dev = BatchedConvexQPSolver(p, self.H, 1, device)
+        # one QP per call: the dual active-set kernel has the lower latency (no batch tail)
+        self._dev = BatchedConvexQPSolver(p, self.H, 1, device, dense_path="gi")
         self._rec = np.zeros((1, 33 + 12 * self.H))
         self._con = np.ones((1, self.H, 4), dtype=np.uint8)
         self.last_status = 0

@@ -399,6 +399,31 @@ def test_dense_path_edge_cases(mode, monkeypatch):
     assert np.all(g[2] == 0.0)
 
 
+def test_dense_path_api(monkeypatch):
+    """lmpc_set_dense_path selects the dense kernel per context (ABI 3); the environment overrides it;
+    H > 16 has no dense path; all paths give the same optimum."""
+    monkeypatch.delenv("LMPC_DENSE", raising=False)
+    p, H, rec, con = synth.config_batch(2, count=64, first_index=9000)
+    out = {}
+    for path in ("ipm", "gi", "off"):
+        s = BatchedConvexQPSolver(p, H, max_batch=64, dense_path=path)
+        assert s.dense_path == path
+        out[path] = s.solve(rec, con)
+    ref, _, _ = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
+    for path, (g, st, it) in out.items():
+        assert np.all(st == 0) and rel_err(g, ref) <= TOL_REGRESS, path
+    assert np.array_equal(out["ipm"][2], out["off"][2])                 # same Newton systems
+    assert not np.array_equal(out["gi"][2], out["ipm"][2])              # active-set steps instead
+    monkeypatch.setenv("LMPC_DENSE", "0")
+    assert BatchedConvexQPSolver(p, H, max_batch=4, dense_path="gi").dense_path == "off"
+    monkeypatch.delenv("LMPC_DENSE")
+    p30, H30, _, _ = synth.config_batch(5, count=1)
+    assert BatchedConvexQPSolver(p30, H30, max_batch=1, dense_path="gi").dense_path == "off"
+    # the single-QP mirror (ConvexMpc drop-in) runs the dual active set
+    from legged_mpc_control_amd import ConvexQPSolver
+    assert ConvexQPSolver(p.q_weights, p.r_weights, horizon=10)._dev.dense_path == "gi"
+
+
 def test_gi_step_cap_hands_over_to_riccati(monkeypatch):
     """A dual active-set QP that reaches the step cap is solved by the Riccati kernel in the same
     launch: same optimum, and its iteration word carries the interior-point counts (polish rounds
