@@ -429,6 +429,12 @@ __global__ void __launch_bounds__(64) lmpc_gi_kernel(const DevParams prm, const 
             if (lane < q) uu = fma(-ts, rk, uu);
             uuq += ts;
             if (zfree && ts == t2) {
+                // at most 3 independent faces per leg-step, so q <= 60 in exact arithmetic; the cap keeps
+                // R^-1 (packed, 64 columns) and the Givens buffer inside their LDS regions regardless
+                if (q >= 3 * DENSE_MAX_LS) {
+                    ok = false;
+                    break;
+                }
                 // ---- add p: Householder on J's columns q.. so that d2 -> |d2| e_q ----
                 const double nrm = sqrt(dd2);
                 if (tail > 0.0) {
