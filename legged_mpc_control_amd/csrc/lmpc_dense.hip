@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                     if (dz[i] < 0.0) amax = fmin(amax, -z[i] * __builtin_amdgcn_rcp(dz[i]));
                 }
             }
-            const double alpha = fmin(1.0, 0.99 * wave_min(amax));
+            const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
             if (st) {
 #pragma unroll
                 for (int m = 0; m < 3; ++m) f[m] += alpha * (u[m] - f[m]);

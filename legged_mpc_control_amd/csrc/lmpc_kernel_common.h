@@ -15,6 +15,10 @@ namespace lmpc {
 // "barrier" is a release/acquire fence pair at wavefront scope around a code-motion barrier.  Unlike
 // __syncthreads() it emits no s_waitcnt lgkmcnt(0): loads issued ahead (prefetches) stay in flight.
 constexpr int LMPC_WAVE = 64;
+// interior point: fraction of the step to the boundary (tools/variant_sweep.py builds other values)
+#ifndef LMPC_STEP_FRAC
+#define LMPC_STEP_FRAC 0.99
+#endif
 #define LMPC_SYNC()                                              \
     do {                                                         \
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \

@@ -1133,7 +1133,7 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                         if (dz[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dz[t][i]));
                     }
                 }
-                const double alpha = fmin(1.0, 0.99 * wave_min(amax));
+                const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
 #pragma unroll
                 for (int t = 0; t < LS; ++t) {
                     if (!st[t]) continue;
