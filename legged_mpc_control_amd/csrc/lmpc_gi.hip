@@ -134,12 +134,12 @@ __device__ __forceinline__ Chunk8 ld_chunk(const ld2* v2, int c) {
     return k;
 }
 
-// Dot of the register row with an LDS vector over columns >= c_lo (the vector is zero below c_lo),
-// 4 independent chains.  Chunk k+1's loads are issued before chunk k's FMAs into a static double
-// buffer (no register copies).
-__device__ __forceinline__ double row_dot(const double (&Jr)[64], const ldouble* v, int c_lo) {
+// Dot of the register row with an LDS vector (zero below the first inactive column q), 4 independent
+// chains, all 64 columns: a uniform branch per chunk to skip those below q cost more (waits at the block
+// joins) than it saved.  Chunk k+1's loads are issued before chunk k's FMAs into a static double buffer
+// (no register copies).
+__device__ __forceinline__ double row_dot(const double (&Jr)[64], const ldouble* v) {
     const ld2* v2 = (const ld2*)v;
-    (void)c_lo;  // no chunk skipping: a uniform branch per chunk costs more (waits at the joins) than it saves
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     Chunk8 buf[2];
     buf[0] = ld_chunk(v2, 0);
@@ -166,10 +166,9 @@ __device__ __forceinline__ double row_dot(const double (&Jr)[64], const ldouble*
     }
     return pin((a0 + a1) + (a2 + a3));
 }
-// Jr -= w * v over columns >= c_lo (v zero below c_lo), pipelined like row_dot
-__device__ __forceinline__ void row_axpy(double (&Jr)[64], double w, const ldouble* v, int c_lo) {
+// Jr -= w * v (v zero below q), pipelined like row_dot
+__device__ __forceinline__ void row_axpy(double (&Jr)[64], double w, const ldouble* v) {
     const ld2* v2 = (const ld2*)v;
-    (void)c_lo;
     Chunk8 buf[2];
     buf[0] = ld_chunk(v2, 0);
 #pragma unroll
@@ -381,7 +380,7 @@ __global__ void __launch_bounds__(64) lmpc_gi_kernel(const DevParams prm, const 
             LMPC_SYNC();
             GSTAMP(3);  // d = J'n, norms
             // ---- z = J2 d2 (lane i = variable i) ----
-            const double z = row_dot(Jr, G.dm, q);
+            const double z = row_dot(Jr, G.dm);
             // ---- r = R^-1 d1 (lane k < q): independent products, no serial chain; the loads of the next
             //      group of 8 columns are issued before this group's FMAs ----
             double rk;
@@ -443,8 +442,8 @@ __global__ void __launch_bounds__(64) lmpc_gi_kernel(const DevParams prm, const 
                     const double beta = 2.0 / (v0 * v0 + tail);
                     G.hv[lane] = lane > q ? dc : lane == q ? v0 : 0.0;
                     LMPC_SYNC();
-                    const double w = beta * row_dot(Jr, G.hv, q);
-                    row_axpy(Jr, w, G.hv, q);
+                    const double w = beta * row_dot(Jr, G.hv);
+                    row_axpy(Jr, w, G.hv);
                 }
                 // R^-1 column q = (-r / |d2|, 1 / |d2|)
                 const double inrm = 1.0 / nrm;
