@@ -26,6 +26,15 @@ constexpr int LMPC_WAVE = 64;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
     } while (0)
 
+// LMPC_SYNC that also orders the wave's global (per-QP scratch) stores before its later loads of the
+// same words by other lanes (workgroup scope = s_waitcnt vmcnt(0) here: one wave per workgroup)
+#define LMPC_GSYNC()                                             \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   \
+    } while (0)
+
 // Explicit LDS address space: every shared access compiles to ds_read/ds_write
 // (a generic pointer would fall back to flat_load/flat_store).
 typedef __attribute__((address_space(3))) double ldouble;

@@ -76,30 +76,34 @@ __device__ __forceinline__ void unpk(int e, int& r, int& c) {
 }
 
 // ---- LDS layout (doubles) --------------------------------------------------
-// per-stage slot
-constexpr int SO_RR = 0;     // 4 x 3x3 input Hessian blocks T'RtT
-constexpr int SO_BT = 36;    // 6 x 12 Bt = G0 T
-constexpr int SO_DV = 108;   // 6   d_k[6:12] = G0 up - g dt e5
-constexpr int SO_RRV = 114;  // 12  input linear term rr (later: y)
-constexpr int SO_N = 126;    // 12 x 12 closed-loop N_k = A_k - [0; K Z]
-constexpr int SO_VV = 270;   // 12  v = P_{k+1} d_k
-constexpr int SO_CST = 282;  // 12  q_k - Z' psi + N' v
-constexpr int SO_PSI = 294;  // 6   V' L^-1 rr
-constexpr int SO_RHO = 300;  // 12  L^-1 rr (later: t)
-constexpr int SO_N6 = 312;   // 6   K s2 + psi - dv (later: q2)
-constexpr int SO_PN = 318;   // 12  p_{k+1}
-constexpr int SO_XS = 330;   // 12  x_k
-constexpr int SO_LAM = 342;  // 12  lambda_{k+1}
-constexpr int SO_ACT = 354;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
-constexpr int SO_LINV = 358; // 78  L^-1 of Guu, row-packed (LDS-resident: the vector pass reads it twice)
-constexpr int SO_ZERO = 436; // 2   always 0.0: target of out-of-range operand offsets
-constexpr int SK = 438;
+// per-stage slot: only what the serial sweeps and the stage-parallel levels read at LDS latency.
+// 180 doubles, so that 3 QPs share a CU at H = 30 and 4 at H = 20 (the matrices the factorisation
+// streams -- Bt, the input Hessian blocks, L^-1 -- live in the per-QP global scratch below and are
+// fetched one stage ahead).
+constexpr int SO_DV = 0;     // 6   d_k[6:12] = G0 up - g dt e5
+constexpr int SO_RRV = 6;    // 12  input linear term rr (later: y)
+constexpr int SO_KZ = 18;    // 6 x 12 rows 6-11 of K^Z^: closed loop N_k = A_k - [0; KZ] (A_k from the yaw)
+constexpr int SO_VV = 90;    // 12  v = P_{k+1} d_k
+constexpr int SO_CST = 102;  // 12  q_k - Z' psi + N' v
+constexpr int SO_PSI = 114;  // 6   V' L^-1 rr
+constexpr int SO_RHO = 120;  // 12  L^-1 rr (later: t)
+constexpr int SO_N6 = 132;   // 6   K s2 + psi - dv (later: q2)
+constexpr int SO_PN = 138;   // 12  p_{k+1}
+constexpr int SO_XS = 150;   // 12  x_k
+constexpr int SO_LAM = 162;  // 12  lambda_{k+1}
+constexpr int SO_ACT = 174;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
+constexpr int SO_ZERO = 178; // 2   always 0.0: target of out-of-range operand offsets
+constexpr int SK = 180;
 // global scratch per stage
 constexpr int GO_V = 0;      // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
 constexpr int GO_K = 72;     // 6 x 6 K = V'V
 constexpr int GO_Z = 108;    // 6 x 12 Z = P2_{k+1} A_k
-constexpr int GO_DUMMY = 180;  // sink for the branch-free masked stores
-constexpr int GS = 182;
+constexpr int GO_BT = 180;   // 6 x 12 Bt = G0 T
+constexpr int GO_RR = 252;   // 4 x 3x3 input Hessian blocks T'RtT
+constexpr int GO_LINV = 288; // 78  L^-1 of Guu, row-packed
+constexpr int GO_ZERO = 366; // 2   always 0.0
+constexpr int GO_DUMMY = 368;  // sink for the branch-free masked stores
+constexpr int GS = 370;
 
 struct Smem {
     ldouble* G0;   // 72
@@ -202,6 +206,28 @@ __device__ __forceinline__ double dtN_entry(int r, int c, double ck, double sk, 
     return v;
 }
 
+// Entry (j, c) of the closed-loop N_k = A_k - [0; KZ] as a lane-static affine form in the stage's
+// yaw (ck, sk) and kzv = KZ[j-6][c]:  N = b + cc ck + sc sk - kz kzv.
+struct NCoef {
+    double b, cc, sc, kz;
+};
+__device__ __forceinline__ NCoef n_coef(int j, int c, double dt) {
+    NCoef n;
+    n.b = (j == c) ? 1.0 : 0.0;
+    n.cc = n.sc = n.kz = 0.0;
+    if (j < 6) {
+        n.b += dtN_entry(j, c, 0.0, 0.0, dt);           // the yaw-independent part
+        n.cc = dtN_entry(j, c, 1.0, 0.0, dt) - (n.b - ((j == c) ? 1.0 : 0.0));
+        n.sc = dtN_entry(j, c, 0.0, 1.0, dt) - (n.b - ((j == c) ? 1.0 : 0.0));
+    } else {
+        n.kz = 1.0;
+    }
+    return n;
+}
+__device__ __forceinline__ double n_eval(const NCoef& n, double ck, double sk, double kzv) {
+    return fma(n.cc, ck, fma(n.sc, sk, fma(-n.kz, kzv, n.b)));
+}
+
 __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, const int H, const double dt,
                                                          const int lane) {
     const int lc = lane & 15, lr = lane >> 4;  // accumulator layout: column lc, rows lr + 4i
@@ -227,33 +253,69 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         }
         if (r >= 3 && r < 6 && c == r + 6) n1[kk] = dt;
     }
-    // B^ (k-blocks 1-2) and Rr operand offsets in the stage slot; out-of-range -> the zero word
-    int boff[2], roff[4];
+    // B^ (k-blocks 1-2: Bt from the global scratch, dv from the stage slot) and Rr operand offsets;
+    // out-of-range -> the zero words
+    int boff[2], dvoff[2], roff[4];
 #pragma unroll
     for (int kk = 1; kk < 3; ++kk) {
         const int r = 4 * kk + lr;
-        boff[kk - 1] = (r >= 6 && r < 12) ? ((lc < 12) ? SO_BT + (r - 6) * 12 + lc : (lc == 12) ? SO_DV + (r - 6) : SO_ZERO)
-                                          : SO_ZERO;
+        const bool brow = r >= 6 && r < 12;
+        boff[kk - 1] = (brow && lc < 12) ? GO_BT + (r - 6) * 12 + lc : GO_ZERO;
+        dvoff[kk - 1] = (brow && lc == 12) ? SO_DV + (r - 6) : SO_ZERO;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = lr + 4 * i;
-        roff[i] = (r < 12 && lc < 12 && (r / 3) == (lc / 3)) ? SO_RR + (r / 3) * 9 + (r % 3) * 3 + (lc % 3) : SO_ZERO;
+        roff[i] = (r < 12 && lc < 12 && (r / 3) == (lc / 3)) ? GO_RR + (r / 3) * 9 + (r % 3) * 3 + (lc % 3) : GO_ZERO;
     }
     // K^ operand: column lc-6 of V for lc in 6-11, else the zero block
     const ldouble* vop = (lc >= 6 && lc < 12) ? S.VL + (lc - 6) * 12 + lr : S.zero;
+    // row m of Bt for the elimination lanes 12-17 (others: row 0, blended out)
+    const int btrow = GO_BT + 12 * ((lane >= 12 && lane < 18) ? lane - 12 : 0);
+    const double btkeep = (lane >= 12 && lane < 18) ? 1.0 : 0.0;
+    // the global operands of a stage do not depend on P: fetched one stage ahead, their latency
+    // hides behind the previous stage's products
+    double bgn[2], rgn[4], btn[12];
+    auto fetch = [&](const gdouble* g) {
+        bgn[0] = g[boff[0]];
+        bgn[1] = g[boff[1]];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rgn[i] = g[roff[i]];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) btn[r] = g[btrow + r];
+    };
+    fetch(gs + (H - 1) * GS);
+    // lane-static destinations of the elimination output (hoisted so the stores stay branch-free)
+    int oofs[12];
+    ldouble* vl;
+    int vstep;
+    {
+        const bool isv = lane >= 12 && lane < 18, isl = lane >= 18 && lane < 30;
+        const int m = isv ? lane - 12 : 0, c = isl ? lane - 18 : 0;
+#pragma unroll
+        for (int r = 0; r < 12; ++r)
+            oofs[r] = isv ? GO_V + m * 12 + r : (isl && r >= c) ? GO_LINV + r * (r + 1) / 2 + c : GO_DUMMY;
+        vl = isv ? S.VL + m * 12 : S.pb;
+        vstep = isv ? 1 : 0;
+    }
     SUB_DECL
     for (int k = H - 1; k >= 0; --k) {
         const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
         ldouble* sl = S.st + k * SK;
         gdouble* g = gs + k * GS;
-        const ldouble* Bt = sl + SO_BT;
+        double bg[2], rg[4], bt[12];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) bg[i] = bgn[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rg[i] = rgn[i];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) bt[r] = btn[r];
         // ---- operands: dt N(yaw) (k-blocks 0-1: rows 0-7) and B^ (k-blocks 1-2) ----
         double nh[2], bh[2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) nh[kk] = fma(nc[kk], ck, fma(ns[kk], sk, n1[kk]));
-        bh[0] = sl[boff[0]];
-        bh[1] = sl[boff[1]];
+        bh[0] = bg[0] + sl[dvoff[0]];
+        bh[1] = bg[1] + sl[dvoff[1]];
         // ---- C^ = P B^ ; PA = P A_k = P + P (dt N) ----
         d4 C = {0.0, 0.0, 0.0, 0.0};
         C = MFMA64(P[1], bh[0], C);
@@ -264,9 +326,13 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         // ---- Guu = Rr + B^' C^ (Rr: 3x3 leg blocks on the diagonal) ----
         d4 G;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) G[i] = sl[roff[i]];
+        for (int i = 0; i < 4; ++i) G[i] = rg[i];
         G = MFMA64(bh[0], C[1], G);
         G = MFMA64(bh[1], C[2], G);
+        // next stage's global operands: issued while the matrix cores work through the chain above
+        __builtin_amdgcn_sched_barrier(0);
+        fetch(gs + (k > 0 ? k - 1 : 0) * GS);
+        __builtin_amdgcn_sched_barrier(0);
         // ---- out: v = C^[:, 12], Guu column-major for the elimination, Z = rows 6-11 of PA ----
         if (lc < 12) {
 #pragma unroll
@@ -288,10 +354,10 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         // from the rows below, reading G_rb straight from the pivot columns.
         double a[12];
         {
-            const ldouble* src = (lane < 12) ? S.GT + 12 * lane : Bt + 12 * (lane < 18 ? lane - 12 : 0);
-            const double keep = (lane < 18) ? 1.0 : 0.0;  // blend, not select: keeps the loads unconditional
+            const ldouble* src = S.GT + 12 * (lane < 12 ? lane : 0);
+            const double keep = (lane < 12) ? 1.0 : 0.0;  // blend, not select: keeps the loads unconditional
 #pragma unroll
-            for (int r = 0; r < 12; ++r) a[r] = fma(src[r], keep, (r == lane - 18) ? 1.0 : 0.0);
+            for (int r = 0; r < 12; ++r) a[r] = fma(src[r], keep, fma(bt[r], btkeep, (r == lane - 18) ? 1.0 : 0.0));
         }
         // Leg blocks with T = 0 (swing legs; apex legs in the polish) have Guu block = I and no
         // coupling (their Bt columns and off-diagonal Rr are exactly zero): their elimination step
@@ -352,20 +418,12 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
             par ^= 1;
             SUB(9 + blk);
         }
-        // out, branch-free: lanes 12-17 -> V (LDS + global), lanes 18-29 -> packed L^-1 into the stage
-        // slot (upper-triangle entries and idle lanes go to dummy words)
-        {
-            const bool isv = lane >= 12 && lane < 18, isl = lane >= 18 && lane < 30;
-            const int m = isv ? lane - 12 : 0, c = isl ? lane - 18 : 0;
-            // one LDS destination per lane and row: V -> VL (for K^), L^-1 -> the stage slot, else a dummy word
-            ldouble* vl = S.VL + m * 12;
-            ldouble* li = sl + SO_LINV + c;
+        // out, branch-free: lanes 12-17 -> V (global, and LDS for K^), lanes 18-29 -> packed L^-1
+        // (global); upper-triangle entries and idle lanes go to dummy words
 #pragma unroll
-            for (int r = 0; r < 12; ++r) {
-                g[isv ? GO_V + m * 12 + r : GO_DUMMY] = a[r];
-                ldouble* ld = isv ? vl + r : (isl && r >= c) ? li + r * (r + 1) / 2 : S.pb;
-                *ld = a[r];
-            }
+        for (int r = 0; r < 12; ++r) {
+            g[oofs[r]] = a[r];
+            vl[r * vstep] = a[r];
         }
         LMPC_SYNC();
         SUB(7);
@@ -380,7 +438,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         d4 KZ = {0.0, 0.0, 0.0, 0.0};
         KZ = MFMA64(KH[1], PA[1], KZ);
         KZ = MFMA64(KH[2], PA[2], KZ);
-        // K -> global (for the vector pass), N_k = A_k - KZ^ -> stage slot
+        // K -> global (for the vector pass), rows 6-11 of KZ^ -> stage slot (N_k = A_k - [0; KZ])
         if (lc >= 6 && lc < 12) {
 #pragma unroll
             for (int i = 1; i < 3; ++i) {
@@ -390,10 +448,9 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         }
         if (lc < 12) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
+            for (int i = 1; i < 3; ++i) {
                 const int r = lr + 4 * i;
-                const double av = ((r == lc) ? 1.0 : 0.0) + (i < 2 ? nh[i < 2 ? i : 0] : 0.0);  // A_k = I + dt N
-                sl[SO_N + r * 12 + lc] = av - KZ[i];
+                if (r >= 6) sl[SO_KZ + (r - 6) * 12 + lc] = KZ[i];
             }
         }
         // ---- P_k = Q + A'PA - PA' KZ^,  A'PA = PA + (dt N)' PA ----
@@ -407,6 +464,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         }
         SUB(8);
     }
+    LMPC_GSYNC();  // V, K, Z, L^-1 in the global scratch visible to every lane of the vector pass
 }
 
 // ---------------------------------------------------------------------------
@@ -465,10 +523,10 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
     for (int i = 0; i < NT12; ++i) {
         const ldouble* rr = S.st + k12[i] * SK + SO_RRV;
-        const ldouble* Li = S.st + k12[i] * SK + SO_LINV + pk(r12[i], 0);  // pk(r, c) < 78 for every c < 12
+        const gdouble* Li = gs + k12[i] * GS + GO_LINV + pk(r12[i], 0);  // pk(r, c) < 78 for every c < 12
         double v = 0.0;
 #pragma unroll
-        for (int c = 0; c < 12; ++c) v += ((c <= r12[i]) ? Li[c] : 0.0) * rr[c];
+        for (int c = 0; c < 12; ++c) v += Li[c] * ((c <= r12[i]) ? rr[c] : 0.0);  // unconditional global loads
         if (v12[i]) S.st[k12[i] * SK + SO_RHO + r12[i]] = v;
     }
     LMPC_SYNC();
@@ -490,8 +548,10 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
         double v = -S.qw[r] * S.xr[(k > 0 ? k - 1 : 0) * 12 + r];
 #pragma unroll
         for (int m = 0; m < 6; ++m) v -= zc[i][m] * sl[SO_PSI + m];
+        // N_k' v = A_k' v - KZ' v[6:12]
+        v += Atw_el(sl + SO_VV, r, S.cs[2 * k], S.cs[2 * k + 1], dt);
 #pragma unroll
-        for (int j = 0; j < 12; ++j) v += sl[SO_N + j * 12 + r] * sl[SO_VV + j];
+        for (int m = 0; m < 6; ++m) v -= sl[SO_KZ + m * 12 + r] * sl[SO_VV + 6 + m];
         if (v12[i] && k > 0) S.st[k * SK + SO_CST + r] = v;
     }
     if (lane < 12) S.st[(H - 1) * SK + SO_PN + lane] = -S.qw[lane] * S.xr[(H - 1) * 12 + lane];
@@ -506,24 +566,42 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
     SUB(0);
     // ---- backward: p_k = N_k' p_{k+1} + cst'_k (into stage k-1's PN slot).  Row r is split over the
     // 4 lanes (r, part): each sums 3 of the 12 terms, a DPP quad reduction combines them.  The lane's
-    // 3 entries of N_k are fetched one step ahead, so only 3 broadcast reads of p_{k+1} sit on the
-    // critical path ----
+    // 3 entries of N_k (column r: rows j0..j0+2) are formed one step ahead -- from the yaw for rows
+    // 0-5, from KZ for rows 6-11 -- so only 3 broadcast reads of p_{k+1} sit on the critical path ----
     {
         const int r = (lane < 48) ? (lane >> 2) : 0, part = lane & 3, j0 = 3 * part;
         const bool wr = lane < 48 && part == 0;
-        double nc[3];
+        const int kzo = SO_KZ + (j0 >= 6 ? j0 - 6 : 0) * 12 + r;  // KZ[j0-6+q][r] at kzo + 12q (rows 6-11)
+        NCoef co[3];
+        double nc[3], rw[5];  // rw: raw operands (yaw cos/sin, 3 KZ entries) of the stage after next
+        const int k1 = H > 1 ? H - 2 : 0;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) nc[q] = S.st[(H - 1) * SK + SO_N + (j0 + q) * 12 + r];
+        for (int q = 0; q < 3; ++q) {
+            co[q] = n_coef(j0 + q, r, dt);
+            nc[q] = n_eval(co[q], S.cs[2 * (H - 1)], S.cs[2 * (H - 1) + 1], S.st[(H - 1) * SK + kzo + 12 * q]);
+        }
+        rw[0] = S.cs[2 * k1];
+        rw[1] = S.cs[2 * k1 + 1];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) rw[2 + q] = S.st[k1 * SK + kzo + 12 * q];
         for (int k = H - 1; k >= 1; --k) {
             const ldouble* sl = S.st + k * SK;
             double pv[3];
 #pragma unroll
             for (int q = 0; q < 3; ++q) pv[q] = sl[SO_PN + j0 + q];
             const double cst = sl[SO_CST + r];
+            // N_{k-1} from the raw operands fetched last step, and the raw operands of k-2, both
+            // while the reads of p_{k+1} are in flight (pinned: the chain below stays clear)
+            __builtin_amdgcn_sched_barrier(0);
             double nn[3];
-            const ldouble* nxt = S.st + (k > 1 ? k - 1 : 1) * SK + SO_N + r;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) nn[q] = nxt[(j0 + q) * 12];
+            for (int q = 0; q < 3; ++q) nn[q] = n_eval(co[q], rw[0], rw[1], rw[2 + q]);
+            const int k2 = k > 2 ? k - 2 : 0;
+            rw[0] = S.cs[2 * k2];
+            rw[1] = S.cs[2 * k2 + 1];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rw[2 + q] = S.st[k2 * SK + kzo + 12 * q];
+            __builtin_amdgcn_sched_barrier(0);
             double v = nc[0] * pv[0] + nc[1] * pv[1] + nc[2] * pv[2];
             v = quad_sum(v);
             ldouble* dst = wr ? S.st + (k - 1) * SK + SO_PN + r : S.pa;  // branch-free: others write a dummy word
@@ -566,9 +644,19 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
         const bool wr = lane < 48 && part == 0;
         const int r6 = (r >= 6) ? r - 6 : 0;
         const double sel = (r >= 6) ? 1.0 : 0.0;
-        double nr[3];
+        const int kzo = SO_KZ + r6 * 12 + j0;  // KZ[r-6][j0+q] (rows 6-11)
+        NCoef co[3];
+        double nr[3], rw[5];  // rw: raw operands of the stage after next (as in the backward sweep)
+        const int k1 = H > 1 ? 1 : 0;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) nr[q] = S.st[SO_N + r * 12 + j0 + q];
+        for (int q = 0; q < 3; ++q) {
+            co[q] = n_coef(r, j0 + q, dt);
+            nr[q] = n_eval(co[q], S.cs[0], S.cs[1], S.st[kzo + q]);
+        }
+        rw[0] = S.cs[2 * k1];
+        rw[1] = S.cs[2 * k1 + 1];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) rw[2 + q] = S.st[k1 * SK + kzo + q];
         for (int k = 0; k < H; ++k) {
             const ldouble* sl = S.st + k * SK;
             ldouble* xo = (k + 1 < H) ? S.st + (k + 1) * SK + SO_XS : S.xH;
@@ -576,10 +664,16 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
             for (int q = 0; q < 3; ++q) x[q] = sl[SO_XS + j0 + q];
             const double n6 = sl[SO_N6 + r6];
+            __builtin_amdgcn_sched_barrier(0);
             double nn[3];
-            const ldouble* nxt = S.st + (k + 1 < H ? k + 1 : k) * SK + SO_N + r * 12 + j0;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) nn[q] = nxt[q];
+            for (int q = 0; q < 3; ++q) nn[q] = n_eval(co[q], rw[0], rw[1], rw[2 + q]);
+            const int k2 = k + 2 < H ? k + 2 : H - 1;
+            rw[0] = S.cs[2 * k2];
+            rw[1] = S.cs[2 * k2 + 1];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rw[2 + q] = S.st[k2 * SK + kzo + q];
+            __builtin_amdgcn_sched_barrier(0);
             double v = nr[0] * x[0] + nr[1] * x[1] + nr[2] * x[2];
             v = quad_sum(v);
             ldouble* dst = wr ? xo + r : S.pa;
@@ -614,10 +708,10 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
     for (int i = 0; i < NT12; ++i) {
         const ldouble* t = S.st + k12[i] * SK + SO_RHO;
-        const ldouble* Li = S.st + k12[i] * SK + SO_LINV;
+        const gdouble* Li = gs + k12[i] * GS + GO_LINV;
         double v = 0.0;
 #pragma unroll
-        for (int r = 0; r < 12; ++r) v += ((r >= r12[i]) ? Li[pk(r, r12[i])] : 0.0) * t[r];  // pk < 78 for all r
+        for (int r = 0; r < 12; ++r) v += Li[pk(r, r12[i])] * ((r >= r12[i]) ? t[r] : 0.0);  // pk < 78 for all r
         if (v12[i]) S.st[k12[i] * SK + SO_RRV + r12[i]] = -v;
     }
     LMPC_SYNC();
@@ -645,7 +739,7 @@ __device__ __forceinline__ void adjoint(const DevParams& prm, const Smem& S, int
 // Interior-point stage data: T = I (stance) / 0 (swing), up = 0, so Rr = Rt (identity for a swing
 // leg), Bt = G0_j masked by contact, dv = -g dt e5.
 template <int LS>
-__device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const Smem& S, const bool (&valid)[LS],
+__device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const Smem& S, gdouble* gs, const bool (&valid)[LS],
                                                    const bool (&st)[LS], const int (&lsk)[LS], const int (&lsj)[LS],
                                                    const double (&Rt)[LS][6]) {
 #pragma unroll
@@ -653,15 +747,16 @@ __device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const S
         if (!valid[t]) continue;
         const int k = lsk[t], j = lsj[t];
         ldouble* sl = S.st + k * SK;
+        gdouble* gl = gs + k * GS;
         const double on = st[t] ? 1.0 : 0.0, off = 1.0 - on;
         const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
 #pragma unroll
-        for (int e = 0; e < 9; ++e) sl[SO_RR + j * 9 + e] = on * R3[e] + ((e % 4 == 0) ? off : 0.0);
+        for (int e = 0; e < 9; ++e) gl[GO_RR + j * 9 + e] = on * R3[e] + ((e % 4 == 0) ? off : 0.0);
         sl[SO_ACT + j] = on;
 #pragma unroll
         for (int m = 0; m < 6; ++m)
 #pragma unroll
-            for (int a = 0; a < 3; ++a) sl[SO_BT + m * 12 + 3 * j + a] = on * S.G0[m * 12 + 3 * j + a];
+            for (int a = 0; a < 3; ++a) gl[GO_BT + m * 12 + 3 * j + a] = on * S.G0[m * 12 + 3 * j + a];
         if (j == 0) {
 #pragma unroll
             for (int m = 0; m < 6; ++m) sl[SO_DV + m] = (m == 5) ? -prm.grav * prm.dt : 0.0;
@@ -672,7 +767,7 @@ __device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const S
 // Per-leg-step stage data: Rr = T'RtT (fixed components -> identity), Bt = G0_j T, dv (quad-reduced).
 // Rt is the symmetric input Hessian block [xx xy xz yy yz zz].  Must be called by ALL lanes.
 template <int LS>
-__device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem& S, const bool (&valid)[LS],
+__device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem& S, gdouble* gs, const bool (&valid)[LS],
                                                const int (&lsk)[LS], const int (&lsj)[LS], const double (&Rt)[LS][6],
                                                const double (&T)[LS][9], const double (&up)[LS][3]) {
 #pragma unroll
@@ -681,6 +776,7 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
         if (valid[t]) {
             const int k = lsk[t], j = lsj[t];
             ldouble* sl = S.st + k * SK;
+            gdouble* gl = gs + k * GS;
             const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
             bool fixed[3];
 #pragma unroll
@@ -698,7 +794,7 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
                 for (int b = 0; b < 3; ++b) {
                     double v = T[t][0 * 3 + a] * RT[0 * 3 + b] + T[t][1 * 3 + a] * RT[1 * 3 + b] + T[t][2 * 3 + a] * RT[2 * 3 + b];
                     if (fixed[a] || fixed[b]) v = (a == b) ? 1.0 : 0.0;
-                    sl[SO_RR + j * 9 + a * 3 + b] = v;
+                    gl[GO_RR + j * 9 + a * 3 + b] = v;
                 }
 #pragma unroll
             for (int m = 0; m < 6; ++m) {
@@ -707,7 +803,7 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
                     double v = 0.0;
 #pragma unroll
                     for (int p = 0; p < 3; ++p) v += S.G0[m * 12 + 3 * j + p] * T[t][p * 3 + a];
-                    sl[SO_BT + m * 12 + 3 * j + a] = v;
+                    gl[GO_BT + m * 12 + 3 * j + a] = v;
                 }
                 double d = 0.0;
 #pragma unroll
@@ -907,7 +1003,10 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     }
     if (lane < 12) S.qw[lane] = prm.q[lane];
     if (lane < 16) S.zero[lane] = 0.0;
-    for (int k = lane; k < H; k += 64) S.st[k * SK + SO_ZERO] = S.st[k * SK + SO_ZERO + 1] = 0.0;
+    for (int k = lane; k < H; k += 64) {
+        S.st[k * SK + SO_ZERO] = S.st[k * SK + SO_ZERO + 1] = 0.0;
+        gs[k * GS + GO_ZERO] = gs[k * GS + GO_ZERO + 1] = 0.0;
+    }
     LMPC_SYNC();
 
     // ---- leg-step ownership and IPM state ----
@@ -1047,11 +1146,11 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
                 }
             }
             SUB(13);  // (diagnostic) leg-step bookkeeping since the previous solve
-            if (mode == PRED) leg_stage_prep_ipm<LS>(prm, S, valid, st, lsk, lsj, Rt);
-            else if (mode == POLISH) leg_stage_prep<LS>(prm, S, valid, lsk, lsj, Rt, T, up);
+            if (mode == PRED) leg_stage_prep_ipm<LS>(prm, S, (gdouble*)gs, valid, st, lsk, lsj, Rt);
+            else if (mode == POLISH) leg_stage_prep<LS>(prm, S, (gdouble*)gs, valid, lsk, lsj, Rt, T, up);
             if (mode == POLISH) leg_rhs<LS>(S, valid, lsk, lsj, Rt, rt, T, up);
             else leg_rhs_ipm<LS>(S, valid, st, lsk, lsj, rt);
-            LMPC_SYNC();
+            LMPC_GSYNC();  // stage data (partly in the global scratch) visible to every lane
             SUB(14);  // (diagnostic) stage prep + rhs
             STAMP(1);  // leg-step work (IPM/polish bookkeeping, stage prep)
             if (mode != CORR) riccati_factor(S, (gdouble*)gs, H, dt, lane);

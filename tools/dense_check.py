@@ -80,6 +80,8 @@ def stamps():
     for i, nm in enumerate(names):
         v = buf[:n, i].astype(float).mean()
         print(f"  {nm:20s} {v:10.0f} ({100 * v / tot.mean():5.1f}%)")
+    print(f"  max cycles/QP {tot.max():.0f}, p99 {np.percentile(tot, 99):.0f}")
+    return tot
 
 
 def gi_stamps():
@@ -107,13 +109,20 @@ def gi_stamps():
           ", ".join(f"{nm} {buf[w, i]}" for i, nm in enumerate(names)))
     per = buf[:n, 2:7].sum(1).astype(float) / np.maximum(steps, 1)
     print(f"  cycles per active-set step: mean {per.mean():.0f}")
+    return tot
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "stamps":
         from legged_mpc_control_amd import build as B
         os.environ["LMPC_LIB"] = B.build_stamps()
-        stamps()
-        gi_stamps()
+        ti = stamps()
+        tg = gi_stamps()
+        both = np.minimum(ti, tg)
+        print(f"per-QP min(ipm, gi): max {both.max():.0f} p99 {np.percentile(both, 99):.0f} mean {both.mean():.0f}; "
+              f"corr(ipm, gi) {np.corrcoef(ti, tg)[0, 1]:.2f}; gi faster on {(tg < ti).sum()}/{len(ti)}")
+        for cap in (300000, 400000, 500000, 600000):
+            c = np.where(tg <= cap, tg, cap + ti)
+            print(f"  gi capped at {cap} cycles then ipm: max {c.max():.0f} mean {c.mean():.0f}")
     else:
         main()
