@@ -141,6 +141,8 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
         const char* gm = std::getenv("LMPC_GI_MAX_STEPS");  // test hook: exercise the hand-over to the Riccati kernel
         c->prm.gi_max_steps = gm ? std::atoi(gm) : 240;
     }
+    if (hipDeviceGetAttribute(&c->prm.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        c->prm.cus = 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return LMPC_ERR_DEVICE;

@@ -25,9 +25,12 @@ struct DevParams {
     int dense;         // QPs with 1..DENSE_MAX_LS stance leg-steps: 0 Riccati kernel, 1 condensed interior
                        // point (lmpc_dense.hip), 2 condensed dual active set (lmpc_gi.hip)
     int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel
+    int cus;           // compute units of the device (launch shaping only)
 };
 constexpr int DENSE_MAX_LS = 20;  // 5 leg-steps per 16-wide tile x 4 tiles (lmpc_dense.hip)
 constexpr int DENSE_MAX_H = 16;   // the dense path's per-step LDS arrays
+
+constexpr size_t LMPC_CU_LDS_BYTES = 160 * 1024;  // LDS per CU on gfx950
 
 // LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
 constexpr int LDS_FIXED_DOUBLES = 464;  // per-QP matrices and buffers

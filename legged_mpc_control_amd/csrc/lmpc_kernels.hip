@@ -228,6 +228,9 @@ __device__ __forceinline__ double n_eval(const NCoef& n, double ck, double sk, d
     return fma(n.cc, ck, fma(n.sc, sk, fma(-n.kz, kzv, n.b)));
 }
 
+// W: the calling kernel's waves-per-SIMD budget -- one copy per budget, so each copy is register-
+// allocated for its caller's occupancy (a shared callee would take the larger budget into both)
+template <int W>
 __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, const int H, const double dt,
                                                          const int lane) {
     const int lc = lane & 15, lr = lane >> 4;  // accumulator layout: column lc, rows lr + 4i
@@ -479,7 +482,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 // the pre-pass data are fetched at entry, the post-pass data at the start of the
 // forward sweep (their L2 latency hides behind the serial recursion).
 // ---------------------------------------------------------------------------
-template <int NT12>
+template <int NT12, int W>
 __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdouble* __restrict__ gs, const int H,
                                                         const double dt, const int lane) {
     constexpr int NT6 = (NT12 + 1) / 2;
@@ -887,8 +890,11 @@ __device__ __forceinline__ void leg_u(const Smem& S, const bool (&valid)[LS], co
 // unchanged on g.  What changes: the input matrix G0 -> G0 blkdiag(R_j), the input Hessian
 // block diag(r_j) -> R_j' diag(r_j) R_j, and the output f = R_j g.  R_j = I for n_j = e_z.
 // ---------------------------------------------------------------------------
-template <int LS, bool TERRAIN>
-__global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const double* __restrict__ rec,
+// WPE = waves per SIMD the register budget allows: 1 (512 VGPR+AGPR per lane, few spills) or 2 (256,
+// some spills).  A lone wave is latency-bound, so a second one per SIMD nearly doubles the issue rate;
+// it needs 8 QPs per CU, which the LDS allows for H <= 10 (launch_qp picks the instance).
+template <int LS, bool TERRAIN, int WPE>
+__global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, const double* __restrict__ rec,
                                                      const uint8_t* __restrict__ contact,
                                                      const double* __restrict__ normals, int batch,
                                                      double* __restrict__ grf, int32_t* __restrict__ status,
@@ -1153,15 +1159,15 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
             LMPC_GSYNC();  // stage data (partly in the global scratch) visible to every lane
             SUB(14);  // (diagnostic) stage prep + rhs
             STAMP(1);  // leg-step work (IPM/polish bookkeeping, stage prep)
-            if (mode != CORR) riccati_factor(S, (gdouble*)gs, H, dt, lane);
+            if (mode != CORR) riccati_factor<WPE>(S, (gdouble*)gs, H, dt, lane);
             STAMP(2);  // factorisation
             switch ((12 * H + 63) / 64) {
-                case 1: riccati_solve<1>(S, (const gdouble*)gs, H, dt, lane); break;
-                case 2: riccati_solve<2>(S, (const gdouble*)gs, H, dt, lane); break;
-                case 3: riccati_solve<3>(S, (const gdouble*)gs, H, dt, lane); break;
-                case 4: riccati_solve<4>(S, (const gdouble*)gs, H, dt, lane); break;
-                case 5: riccati_solve<5>(S, (const gdouble*)gs, H, dt, lane); break;
-                default: riccati_solve<6>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 1: riccati_solve<1, WPE>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 2: riccati_solve<2, WPE>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 3: riccati_solve<3, WPE>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 4: riccati_solve<4, WPE>(S, (const gdouble*)gs, H, dt, lane); break;
+                case 5: riccati_solve<5, WPE>(S, (const gdouble*)gs, H, dt, lane); break;
+                default: riccati_solve<6, WPE>(S, (const gdouble*)gs, H, dt, lane); break;
             }
             STAMP(3);  // vector pass
             SUB(15);   // (diagnostic) factor + solve, already split by their own stamps
@@ -1369,25 +1375,27 @@ __global__ void __launch_bounds__(64) lmpc_qp_kernel(const DevParams prm, const 
     }
 }
 
-#define LMPC_INST(LS_, T_)                                                                                      \
-    template __global__ void lmpc_qp_kernel<LS_, T_>(const DevParams, const double*, const uint8_t*, const double*, \
-                                                     int, double*, int32_t*, int32_t*, double*, const uint8_t*);
-LMPC_INST(1, false)
-LMPC_INST(2, false)
-LMPC_INST(1, true)
-LMPC_INST(2, true)
+#define LMPC_INST(LS_, T_, W_)                                                                                         \
+    template __global__ void lmpc_qp_kernel<LS_, T_, W_>(const DevParams, const double*, const uint8_t*, const double*, \
+                                                         int, double*, int32_t*, int32_t*, double*, const uint8_t*);
+LMPC_INST(1, false, 1)
+LMPC_INST(1, false, 2)
+LMPC_INST(2, false, 1)
+LMPC_INST(1, true, 1)
+LMPC_INST(1, true, 2)
+LMPC_INST(2, true, 1)
 #undef LMPC_INST
 
-template <int LS, bool TERRAIN>
+template <int LS, bool TERRAIN, int WPE>
 static void launch_variant(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                            int batch, double* grf, int32_t* status, int32_t* iters, double* scratch,
                            const uint8_t* done, hipStream_t stream) {
     const size_t lds = lds_bytes(prm.H, TERRAIN);
     const dim3 grid(batch), block(LMPC_WAVE);  // LMPC_SYNC() relies on exactly one wavefront per workgroup
-    (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<LS, TERRAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    hipLaunchKernelGGL((lmpc_qp_kernel<LS, TERRAIN>), grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
-                       status, iters, scratch, done);
+    (void)hipFuncSetAttribute((const void*)lmpc_qp_kernel<LS, TERRAIN, WPE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((lmpc_qp_kernel<LS, TERRAIN, WPE>), grid, block, lds, stream, prm, rec, contact, normals, batch,
+                       grf, status, iters, scratch, done);
 }
 
 // Host-side launcher (called from lmpc_capi.cpp).  normals == nullptr: flat ground (the reference).
@@ -1395,12 +1403,18 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
                      int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, const uint8_t* done,
                      hipStream_t stream) {
     const bool two = 4 * prm.H > 64;
+    // two waves per SIMD when 8 QPs fit the CU's LDS and the batch has more QPs than the device has
+    // SIMDs (up to one QP per SIMD the lone-wave instance, free of spills, is faster).  Same arithmetic,
+    // so the choice never changes a result bit.
+    const bool w2 = !two && 8 * lds_bytes(prm.H, normals != nullptr) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
     if (normals) {
-        if (two) launch_variant<2, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
-        else launch_variant<1, true>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        if (two) launch_variant<2, true, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        else if (w2) launch_variant<1, true, 2>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        else launch_variant<1, true, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
     } else {
-        if (two) launch_variant<2, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
-        else launch_variant<1, false>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        if (two) launch_variant<2, false, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        else if (w2) launch_variant<1, false, 2>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        else launch_variant<1, false, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
     }
     return hipGetLastError();
 }

@@ -83,8 +83,9 @@ def test_full_config2_batch_vs_oracle():
 @pytest.mark.parametrize("cid,mode", [(3, "ipm"), (4, "ipm"), (4, "gi"), (5, "ipm")])
 def test_full_size_properties(cid, mode, torch_dev, monkeypatch):
     """Configs 3/4/5 at full batch: converged, feasible, swing legs exactly zero,
-    bitwise deterministic, permutation-invariant and shard-invariant (config 4 also with the
-    dual active-set kernel on its dense-eligible QPs)."""
+    bitwise deterministic, permutation-invariant and shard-invariant, including a shard small enough
+    to change the Riccati kernel instance (config 4 also with the dual active-set kernel on its
+    dense-eligible QPs)."""
     import torch
 
     monkeypatch.setenv("LMPC_DENSE", mode)
@@ -118,6 +119,13 @@ def test_full_size_properties(cid, mode, torch_dev, monkeypatch):
     s.solve_device(d_rec[half:].contiguous(), d_con[half:].contiguous(), out4, st[: B - half])
     torch.cuda.synchronize()
     assert torch.equal(out4, out[half:])
+    # a shard of at most one QP per SIMD: at H <= 10 the Riccati kernel then runs its one-wave-per-SIMD
+    # instance instead of the two-wave one (launch_qp) -- same arithmetic, same bits
+    small = 512
+    out5 = torch.empty((small, H, 12), dtype=torch.float64, device=torch_dev)
+    s.solve_device(d_rec[:small].contiguous(), d_con[:small].contiguous(), out5, st[:small])
+    torch.cuda.synchronize()
+    assert torch.equal(out5, out[:small])
     # oracle on a sample
     idx = np.random.default_rng(cid).choice(B, 32, replace=False)
     ref, _, _ = O.solve_batch(O.params_from(p), H, rec[idx], con[idx], n_threads=8)
