@@ -231,8 +231,9 @@ __device__ __forceinline__ double n_eval(const NCoef& n, double ck, double sk, d
 // W: the calling kernel's waves-per-SIMD budget -- one copy per budget, so each copy is register-
 // allocated for its caller's occupancy (a shared callee would take the larger budget into both)
 template <int W>
-__device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, const int H, const double dt,
+__device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, int H, const double dt,
                                                          const int lane) {
+    H = __builtin_amdgcn_readfirstlane(H);  // wave-uniform (arguments arrive in VGPRs): scalar loop control
     const int lc = lane & 15, lr = lane >> 4;  // accumulator layout: column lc, rows lr + 4i
     d4 P;
 #pragma unroll
@@ -483,9 +484,10 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 // forward sweep (their L2 latency hides behind the serial recursion).
 // ---------------------------------------------------------------------------
 template <int NT12, int W>
-__device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdouble* __restrict__ gs, const int H,
+__device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdouble* __restrict__ gs, int H,
                                                         const double dt, const int lane) {
     constexpr int NT6 = (NT12 + 1) / 2;
+    H = __builtin_amdgcn_readfirstlane(H);  // wave-uniform (arguments arrive in VGPRs): scalar loop control
     const int n12 = 12 * H, n6 = 6 * H;
     SUB_DECL
     int k12[NT12], r12[NT12];
