@@ -34,7 +34,7 @@ constexpr size_t LMPC_CU_LDS_BYTES = 160 * 1024;  // LDS per CU on gfx950
 
 // LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
 constexpr int LDS_FIXED_DOUBLES = 464;  // per-QP matrices and buffers
-constexpr int LDS_STAGE_DOUBLES = 180;  // per-stage slot (SK)
+constexpr int LDS_STAGE_DOUBLES = 166;  // per-stage slot (SK)
 constexpr int LDS_TERRAIN_DOUBLES = 60;  // terrain extension: 4 contact frames (36) + 4 packed R'diag(r)R (24)
 inline int lds_doubles(int H, bool terrain = false) {
     return LDS_FIXED_DOUBLES + 14 * H + LDS_STAGE_DOUBLES * H + (terrain ? LDS_TERRAIN_DOUBLES : 0);

@@ -77,23 +77,22 @@ __device__ __forceinline__ void unpk(int e, int& r, int& c) {
 
 // ---- LDS layout (doubles) --------------------------------------------------
 // per-stage slot: only what the serial sweeps and the stage-parallel levels read at LDS latency.
-// 180 doubles, so that 3 QPs share a CU at H = 30 and 4 at H = 20 (the matrices the factorisation
+// 166 doubles, so that 3 QPs share a CU at H = 30 and 4 at H = 20 (the matrices the factorisation
 // streams -- Bt, the input Hessian blocks, L^-1 -- live in the per-QP global scratch below and are
 // fetched one stage ahead).
 constexpr int SO_DV = 0;     // 6   d_k[6:12] = G0 up - g dt e5
 constexpr int SO_RRV = 6;    // 12  input linear term rr (later: y)
 constexpr int SO_KZ = 18;    // 6 x 12 rows 6-11 of K^Z^: closed loop N_k = A_k - [0; KZ] (A_k from the yaw)
 constexpr int SO_VV = 90;    // 12  v = P_{k+1} d_k
-constexpr int SO_CST = 102;  // 12  q_k - Z' psi + N' v
+constexpr int SO_CST = 102;  // 12  q_k - Z' psi + N' v (dead after the backward sweep)
+constexpr int SO_LAM = 102;  // 12  lambda_{k+1}: the adjoint after a solve, read before the next one (aliases CST)
 constexpr int SO_PSI = 114;  // 6   V' L^-1 rr
 constexpr int SO_RHO = 120;  // 12  L^-1 rr (later: t)
 constexpr int SO_N6 = 132;   // 6   K s2 + psi - dv (later: q2)
 constexpr int SO_PN = 138;   // 12  p_{k+1}
 constexpr int SO_XS = 150;   // 12  x_k
-constexpr int SO_LAM = 162;  // 12  lambda_{k+1}
-constexpr int SO_ACT = 174;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
-constexpr int SO_ZERO = 178; // 2   always 0.0: target of out-of-range operand offsets
-constexpr int SK = 180;
+constexpr int SO_ACT = 162;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
+constexpr int SK = 166;
 // global scratch per stage
 constexpr int GO_V = 0;      // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
 constexpr int GO_K = 72;     // 6 x 6 K = V'V
@@ -260,12 +259,14 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
     // B^ (k-blocks 1-2: Bt from the global scratch, dv from the stage slot) and Rr operand offsets;
     // out-of-range -> the zero words
     int boff[2], dvoff[2], roff[4];
+    double dvsel[2];  // dv enters column 12 of B^ only (blend, not select: the LDS read stays unconditional)
 #pragma unroll
     for (int kk = 1; kk < 3; ++kk) {
         const int r = 4 * kk + lr;
         const bool brow = r >= 6 && r < 12;
         boff[kk - 1] = (brow && lc < 12) ? GO_BT + (r - 6) * 12 + lc : GO_ZERO;
-        dvoff[kk - 1] = (brow && lc == 12) ? SO_DV + (r - 6) : SO_ZERO;
+        dvoff[kk - 1] = SO_DV + (brow ? r - 6 : 0);
+        dvsel[kk - 1] = (brow && lc == 12) ? 1.0 : 0.0;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -318,8 +319,8 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         double nh[2], bh[2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) nh[kk] = fma(nc[kk], ck, fma(ns[kk], sk, n1[kk]));
-        bh[0] = bg[0] + sl[dvoff[0]];
-        bh[1] = bg[1] + sl[dvoff[1]];
+        bh[0] = fma(dvsel[0], sl[dvoff[0]], bg[0]);
+        bh[1] = fma(dvsel[1], sl[dvoff[1]], bg[1]);
         // ---- C^ = P B^ ; PA = P A_k = P + P (dt N) ----
         d4 C = {0.0, 0.0, 0.0, 0.0};
         C = MFMA64(P[1], bh[0], C);
@@ -894,7 +895,7 @@ __device__ __forceinline__ void leg_u(const Smem& S, const bool (&valid)[LS], co
 // ---------------------------------------------------------------------------
 // WPE = waves per SIMD the register budget allows: 1 (512 VGPR+AGPR per lane, few spills) or 2 (256,
 // some spills).  A lone wave is latency-bound, so a second one per SIMD nearly doubles the issue rate;
-// it needs 8 QPs per CU, which the LDS allows for H <= 10 (launch_qp picks the instance).
+// it pays once the LDS admits more than 4 QPs per CU (H <= 16; launch_qp picks the instance).
 template <int LS, bool TERRAIN, int WPE>
 __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, const double* __restrict__ rec,
                                                      const uint8_t* __restrict__ contact,
@@ -1012,7 +1013,6 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
     if (lane < 12) S.qw[lane] = prm.q[lane];
     if (lane < 16) S.zero[lane] = 0.0;
     for (int k = lane; k < H; k += 64) {
-        S.st[k * SK + SO_ZERO] = S.st[k * SK + SO_ZERO + 1] = 0.0;
         gs[k * GS + GO_ZERO] = gs[k * GS + GO_ZERO + 1] = 0.0;
     }
     LMPC_SYNC();
@@ -1405,19 +1405,21 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
                      int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, const uint8_t* done,
                      hipStream_t stream) {
     const bool two = 4 * prm.H > 64;
-    // two waves per SIMD when 8 QPs fit the CU's LDS and the batch has more QPs than the device has
-    // SIMDs (up to one QP per SIMD the lone-wave instance, free of spills, is faster).  Same arithmetic,
-    // so the choice never changes a result bit.
-    const bool w2 = !two && 8 * lds_bytes(prm.H, normals != nullptr) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
+    // two waves per SIMD when more than 4 QPs fit the CU's LDS and the batch has more QPs than the
+    // device has SIMDs (up to one QP per SIMD the lone-wave instance, free of spills, is faster); H <= 16
+    // only: the LS = 2 state spills too much at 256 registers (measured at H = 20, 5 QPs per CU: 22 %
+    // slower than 4 at one wave per SIMD).  Same arithmetic, so the choice never changes a result bit.
+    const bool w2 = !two && 5 * lds_bytes(prm.H, normals != nullptr) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
+#define LMPC_LAUNCH(LS_, T_, W_) \
+    launch_variant<LS_, T_, W_>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream)
     if (normals) {
-        if (two) launch_variant<2, true, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
-        else if (w2) launch_variant<1, true, 2>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
-        else launch_variant<1, true, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        if (two) LMPC_LAUNCH(2, true, 1);
+        else w2 ? LMPC_LAUNCH(1, true, 2) : LMPC_LAUNCH(1, true, 1);
     } else {
-        if (two) launch_variant<2, false, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
-        else if (w2) launch_variant<1, false, 2>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
-        else launch_variant<1, false, 1>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream);
+        if (two) LMPC_LAUNCH(2, false, 1);
+        else w2 ? LMPC_LAUNCH(1, false, 2) : LMPC_LAUNCH(1, false, 1);
     }
+#undef LMPC_LAUNCH
     return hipGetLastError();
 }
 
