@@ -34,14 +34,14 @@ constexpr size_t LMPC_CU_LDS_BYTES = 160 * 1024;  // LDS per CU on gfx950
 
 // LDS footprint (doubles) of one QP for horizon H; carve() in lmpc_kernels.hip static_asserts both constants.
 constexpr int LDS_FIXED_DOUBLES = 464;  // per-QP matrices and buffers
-constexpr int LDS_STAGE_DOUBLES = 166;  // per-stage slot (SK)
+constexpr int LDS_STAGE_DOUBLES = 150;  // per-stage slot (SK)
 constexpr int LDS_TERRAIN_DOUBLES = 60;  // terrain extension: 4 contact frames (36) + 4 packed R'diag(r)R (24)
 inline int lds_doubles(int H, bool terrain = false) {
-    return LDS_FIXED_DOUBLES + 14 * H + LDS_STAGE_DOUBLES * H + (terrain ? LDS_TERRAIN_DOUBLES : 0);
+    return LDS_FIXED_DOUBLES + 2 * H + LDS_STAGE_DOUBLES * H + (terrain ? LDS_TERRAIN_DOUBLES : 0);
 }
 inline size_t lds_bytes(int H, bool terrain = false) { return (size_t)lds_doubles(H, terrain) * sizeof(double); }
-// Global scratch (doubles) per QP: V, K, Z, Bt, input Hessian blocks, L^-1 per stage (GS in lmpc_kernels.hip, static_asserted).
-constexpr int SCRATCH_STAGE_DOUBLES = 370;
+// Global scratch (doubles) per QP: V, K, Z, Bt, input Hessian blocks, L^-1, dv, leg flags per stage (GS in lmpc_kernels.hip, static_asserted).
+constexpr int SCRATCH_STAGE_DOUBLES = 380;
 inline size_t scratch_doubles_per_qp(int H) { return (size_t)SCRATCH_STAGE_DOUBLES * H; }
 
 }  // namespace lmpc

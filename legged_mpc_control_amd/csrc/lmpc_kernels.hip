@@ -77,22 +77,20 @@ __device__ __forceinline__ void unpk(int e, int& r, int& c) {
 
 // ---- LDS layout (doubles) --------------------------------------------------
 // per-stage slot: only what the serial sweeps and the stage-parallel levels read at LDS latency.
-// 166 doubles, so that 3 QPs share a CU at H = 30 and 4 at H = 20 (the matrices the factorisation
+// 150 doubles, so that 4 QPs share a CU at H = 30 (the matrices the factorisation
 // streams -- Bt, the input Hessian blocks, L^-1 -- live in the per-QP global scratch below and are
 // fetched one stage ahead).
-constexpr int SO_DV = 0;     // 6   d_k[6:12] = G0 up - g dt e5
-constexpr int SO_RRV = 6;    // 12  input linear term rr (later: y)
-constexpr int SO_KZ = 18;    // 6 x 12 rows 6-11 of K^Z^: closed loop N_k = A_k - [0; KZ] (A_k from the yaw)
-constexpr int SO_VV = 90;    // 12  v = P_{k+1} d_k
-constexpr int SO_CST = 102;  // 12  q_k - Z' psi + N' v (dead after the backward sweep)
-constexpr int SO_LAM = 102;  // 12  lambda_{k+1}: the adjoint after a solve, read before the next one (aliases CST)
-constexpr int SO_PSI = 114;  // 6   V' L^-1 rr
-constexpr int SO_RHO = 120;  // 12  L^-1 rr (later: t)
-constexpr int SO_N6 = 132;   // 6   K s2 + psi - dv (later: q2)
-constexpr int SO_PN = 138;   // 12  p_{k+1}
-constexpr int SO_XS = 150;   // 12  x_k
-constexpr int SO_ACT = 162;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
-constexpr int SK = 166;
+constexpr int SO_RRV = 0;    // 12  input linear term rr (later: y)
+constexpr int SO_KZ = 12;    // 6 x 12 rows 6-11 of K^Z^: closed loop N_k = A_k - [0; KZ] (A_k from the yaw)
+constexpr int SO_VV = 84;    // 12  v = P_{k+1} d_k
+constexpr int SO_CST = 96;   // 12  q_k - Z' psi + N' v (dead after the backward sweep)
+constexpr int SO_LAM = 96;   // 12  lambda_{k+1}: the adjoint after a solve, read before the next one (aliases CST)
+constexpr int SO_PSI = 108;  // 6   V' L^-1 rr (dead once the mid level has read it)
+constexpr int SO_N6 = 108;   // 6   K s2 + psi - dv, later q2 (aliases PSI: each mid task reads its own psi entry)
+constexpr int SO_RHO = 114;  // 12  L^-1 rr (later: t)
+constexpr int SO_PN = 126;   // 12  p_{k+1}
+constexpr int SO_XS = 138;   // 12  x_k
+constexpr int SK = 150;
 // global scratch per stage
 constexpr int GO_V = 0;      // 6 x 12 V' (column m of V = L^-1 Bt' contiguous)
 constexpr int GO_K = 72;     // 6 x 6 K = V'V
@@ -100,15 +98,17 @@ constexpr int GO_Z = 108;    // 6 x 12 Z = P2_{k+1} A_k
 constexpr int GO_BT = 180;   // 6 x 12 Bt = G0 T
 constexpr int GO_RR = 252;   // 4 x 3x3 input Hessian blocks T'RtT
 constexpr int GO_LINV = 288; // 78  L^-1 of Guu, row-packed
-constexpr int GO_ZERO = 366; // 2   always 0.0
-constexpr int GO_DUMMY = 368;  // sink for the branch-free masked stores
-constexpr int GS = 370;
+constexpr int GO_DV = 366;   // 6   d_k[6:12] = G0 up - g dt e5
+constexpr int GO_ACT = 372;  // 4   leg block coupled (1) or decoupled identity block (0: T = 0)
+constexpr int GO_ZERO = 376; // 2   always 0.0
+constexpr int GO_DUMMY = 378;  // sink for the branch-free masked stores
+constexpr int GS = 380;
 
 struct Smem {
     ldouble* G0;   // 72
     ldouble* hdr;  // 40: x0(12) R(9) feet(12)
     ldouble* cs;   // 2H
-    ldouble* xr;   // 12H
+    const gdouble* xr;  // 12H x_ref, read from the input record in global memory (L2-resident after first use)
     ldouble* xH;   // 12
     ldouble* GT;   // 144  Guu, column-major
     ldouble* PNL;  // 72   pivot block columns (3 columns x 12 rows), double-buffered
@@ -145,8 +145,8 @@ __device__ __forceinline__ Smem carve(double* sm, int H) {
     s.qw = p; p += 12;
     s.zero = p; p += 16;
     s.cs = p; p += 2 * H;
-    s.xr = p; p += 12 * H;
-    s.st = p;  // offset LDS_FIXED_DOUBLES + 14H doubles (even: 16-B aligned)
+    s.xr = nullptr;  // set by the kernel
+    s.st = p;  // offset LDS_FIXED_DOUBLES + 2H doubles (even: 16-B aligned)
     return s;
 }
 
@@ -258,15 +258,12 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
     }
     // B^ (k-blocks 1-2: Bt from the global scratch, dv from the stage slot) and Rr operand offsets;
     // out-of-range -> the zero words
-    int boff[2], dvoff[2], roff[4];
-    double dvsel[2];  // dv enters column 12 of B^ only (blend, not select: the LDS read stays unconditional)
+    int boff[2], roff[4];
 #pragma unroll
     for (int kk = 1; kk < 3; ++kk) {
         const int r = 4 * kk + lr;
         const bool brow = r >= 6 && r < 12;
-        boff[kk - 1] = (brow && lc < 12) ? GO_BT + (r - 6) * 12 + lc : GO_ZERO;
-        dvoff[kk - 1] = SO_DV + (brow ? r - 6 : 0);
-        dvsel[kk - 1] = (brow && lc == 12) ? 1.0 : 0.0;
+        boff[kk - 1] = (brow && lc < 12) ? GO_BT + (r - 6) * 12 + lc : (brow && lc == 12) ? GO_DV + (r - 6) : GO_ZERO;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -280,10 +277,12 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
     const double btkeep = (lane >= 12 && lane < 18) ? 1.0 : 0.0;
     // the global operands of a stage do not depend on P: fetched one stage ahead, their latency
     // hides behind the previous stage's products
-    double bgn[2], rgn[4], btn[12];
+    double bgn[2], rgn[4], btn[12], agn[4];
     auto fetch = [&](const gdouble* g) {
         bgn[0] = g[boff[0]];
         bgn[1] = g[boff[1]];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) agn[j] = g[GO_ACT + j];
 #pragma unroll
         for (int i = 0; i < 4; ++i) rgn[i] = g[roff[i]];
 #pragma unroll
@@ -308,9 +307,11 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
         ldouble* sl = S.st + k * SK;
         gdouble* g = gs + k * GS;
-        double bg[2], rg[4], bt[12];
+        double bg[2], rg[4], bt[12], ag[4];
 #pragma unroll
         for (int i = 0; i < 2; ++i) bg[i] = bgn[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ag[j] = agn[j];
 #pragma unroll
         for (int i = 0; i < 4; ++i) rg[i] = rgn[i];
 #pragma unroll
@@ -319,8 +320,8 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         double nh[2], bh[2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) nh[kk] = fma(nc[kk], ck, fma(ns[kk], sk, n1[kk]));
-        bh[0] = fma(dvsel[0], sl[dvoff[0]], bg[0]);
-        bh[1] = fma(dvsel[1], sl[dvoff[1]], bg[1]);
+        bh[0] = bg[0];
+        bh[1] = bg[1];
         // ---- C^ = P B^ ; PA = P A_k = P + P (dt N) ----
         d4 C = {0.0, 0.0, 0.0, 0.0};
         C = MFMA64(P[1], bh[0], C);
@@ -369,8 +370,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         // is the identity and is skipped.  amask is wave-uniform (scalar branches).
         int amask;
         {
-            const double f0 = sl[SO_ACT], f1 = sl[SO_ACT + 1], f2 = sl[SO_ACT + 2], f3 = sl[SO_ACT + 3];
-            amask = (f0 != 0.0 ? 1 : 0) | (f1 != 0.0 ? 2 : 0) | (f2 != 0.0 ? 4 : 0) | (f3 != 0.0 ? 8 : 0);
+            amask = (ag[0] != 0.0 ? 1 : 0) | (ag[1] != 0.0 ? 2 : 0) | (ag[2] != 0.0 ? 4 : 0) | (ag[3] != 0.0 ? 8 : 0);
             amask = __builtin_amdgcn_readfirstlane(amask);
         }
         if (amask) {  // pivot columns of the first coupled block
@@ -622,7 +622,7 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 #pragma unroll
     for (int i = 0; i < NT6; ++i) {
         const ldouble* sl = S.st + k6[i] * SK;
-        double v = sl[SO_PSI + m6[i]] - sl[SO_DV + m6[i]];
+        double v = sl[SO_PSI + m6[i]] - gs[k6[i] * GS + GO_DV + m6[i]];
 #pragma unroll
         for (int n = 0; n < 6; ++n) v += kk[i][n] * (sl[SO_VV + 6 + n] + sl[SO_PN + 6 + n]);
         if (v6[i]) S.st[k6[i] * SK + SO_N6 + m6[i]] = v;
@@ -725,18 +725,31 @@ __device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdou
 }
 
 // Adjoint: lambda_{k+1} for every stage (SO_LAM) from the trajectory in SO_XS / xH.
+//   lambda_H = q (x_H - xr_{H-1});  lambda_k = q (x_k - xr_{k-1}) + A_k' lambda_{k+1}
+// The tracking terms do not depend on lambda: one stage-parallel level writes them (x_ref comes from
+// global memory, so its latency is paid once), then the serial sweep adds A_k' lambda_{k+1} in place.
 __device__ __forceinline__ void adjoint(const DevParams& prm, const Smem& S, int lane) {
     const int H = prm.H;
     const double dt = prm.dt;
-    if (lane < 12) S.st[(H - 1) * SK + SO_LAM + lane] = prm.q[lane] * (S.xH[lane] - S.xr[(H - 1) * 12 + lane]);
+    const int n12 = 12 * H;
+    constexpr int MAXT = (12 * 32 + 63) / 64;  // H <= 32
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+        const int e = lane + 64 * i;
+        if (64 * i >= n12) break;  // wave-uniform
+        const int ec = e < n12 ? e : n12 - 1;  // clamped: the load stays unconditional
+        const int k = ec / 12, r = ec - 12 * k;
+        const double xn = (k + 1 < H) ? S.st[(k + 1) * SK + SO_XS + r] : S.xH[r];
+        const double v = prm.q[r] * (xn - S.xr[ec]);
+        if (e < n12) S.st[k * SK + SO_LAM + r] = v;
+    }
     LMPC_SYNC();
     for (int k = H - 1; k >= 1; --k) {
         if (lane < 12) {
             const int r = lane;
             const ldouble* lam = S.st + k * SK + SO_LAM;
             const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
-            S.st[(k - 1) * SK + SO_LAM + r] =
-                prm.q[r] * (S.st[k * SK + SO_XS + r] - S.xr[(k - 1) * 12 + r]) + Atw_el(lam, r, ck, sk, dt);
+            S.st[(k - 1) * SK + SO_LAM + r] += Atw_el(lam, r, ck, sk, dt);
         }
         LMPC_SYNC();
     }
@@ -758,14 +771,14 @@ __device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const S
         const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
 #pragma unroll
         for (int e = 0; e < 9; ++e) gl[GO_RR + j * 9 + e] = on * R3[e] + ((e % 4 == 0) ? off : 0.0);
-        sl[SO_ACT + j] = on;
+        gl[GO_ACT + j] = on;
 #pragma unroll
         for (int m = 0; m < 6; ++m)
 #pragma unroll
             for (int a = 0; a < 3; ++a) gl[GO_BT + m * 12 + 3 * j + a] = on * S.G0[m * 12 + 3 * j + a];
         if (j == 0) {
 #pragma unroll
-            for (int m = 0; m < 6; ++m) sl[SO_DV + m] = (m == 5) ? -prm.grav * prm.dt : 0.0;
+            for (int m = 0; m < 6; ++m) gl[GO_DV + m] = (m == 5) ? -prm.grav * prm.dt : 0.0;
         }
     }
 }
@@ -787,7 +800,7 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
             bool fixed[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) fixed[a] = (T[t][a] == 0.0 && T[t][3 + a] == 0.0 && T[t][6 + a] == 0.0);
-            sl[SO_ACT + j] = (fixed[0] && fixed[1] && fixed[2]) ? 0.0 : 1.0;
+            gl[GO_ACT + j] = (fixed[0] && fixed[1] && fixed[2]) ? 0.0 : 1.0;
             double RT[9];  // Rt T
 #pragma unroll
             for (int p = 0; p < 3; ++p)
@@ -820,9 +833,9 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
 #pragma unroll
         for (int m = 0; m < 6; ++m) du[m] = quad_sum(du[m]);
         if (valid[t] && lsj[t] == 0) {
-            ldouble* sl = S.st + lsk[t] * SK;
+            gdouble* gl = gs + lsk[t] * GS;
 #pragma unroll
-            for (int m = 0; m < 6; ++m) sl[SO_DV + m] = du[m] - (m == 5 ? prm.grav * prm.dt : 0.0);
+            for (int m = 0; m < 6; ++m) gl[GO_DV + m] = du[m] - (m == 5 ? prm.grav * prm.dt : 0.0);
         }
     }
 }
@@ -915,7 +928,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
         if (n >= 1 && n <= DENSE_MAX_LS && (!dense_done || dense_done[qp])) return;
     }
     const int RL = 33 + 12 * H;
-    const Smem S = carve(lmpc_smem, H);
+    Smem S = carve(lmpc_smem, H);
     ldouble* const tf = S.st + SK * H;  // TERRAIN only: R_j (9 each, row-major) | R_j' diag(r_j) R_j packed (6 each)
     double* gs = scratch + (size_t)qp * GS * H;
     const double mu = prm.mu, fzmax = prm.fmax, dt = prm.dt;
@@ -923,11 +936,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
 
     // ---- load the record (coalesced, one pass) ----
     const double* rin = rec + (size_t)qp * RL;
-    for (int i = lane; i < RL; i += 64) {
-        const double v = rin[i];
-        if (i < 33) S.hdr[i] = v;
-        else S.xr[i - 33] = v;
-    }
+    if (lane < 33) S.hdr[lane] = rin[lane];
+    S.xr = (const gdouble*)(rin + 33);
     if constexpr (TERRAIN) {
         if (lane < 4) {
             // contact frame of leg `lane` (same closed form as lmpc_terrain_frame, lmpc_host.cpp)
