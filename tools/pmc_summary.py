@@ -70,7 +70,7 @@ def main():
         }
     json.dump(per, open(os.path.join(DST, "pmc_per_dispatch.json"), "w"), indent=1)
     json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
-    for c in ("c2", "c4", "c2gi"):
+    for c in ("c2", "c4", "c2gi", "c3", "c5"):
         shutil.copy(os.path.join(SRC, c, f"{c}_kernel_stats.csv"), os.path.join(DST, f"{c}_kernel_stats.csv"))
         shutil.copy(os.path.join(SRC, f"{c}_bench.log"), os.path.join(DST, f"{c}_bench.log"))
     for k, v in traffic.items():
