@@ -159,6 +159,26 @@ def test_horizon_range(H):
     assert rel_err(grf, ref) <= TOL_REGRESS
 
 
+@pytest.mark.parametrize("H,mode", [(16, "0"), (16, "ipm"), (12, "gi"), (17, "ipm")])
+def test_riccati_instances_large_batch(H, mode, monkeypatch):
+    """Batches above one QP per SIMD (2048 mixed-gait QPs): at H <= 16 the Riccati kernel runs its two-wave
+    instance, at H = 17 the one-wave two-leg-step instance.  Sampled QPs vs the oracle, and a 256-QP shard
+    (one-wave instance) bit-identical to the same QPs inside the large batch."""
+    monkeypatch.setenv("LMPC_DENSE", mode)
+    p, _, rec, con = synth.config_batch(4, count=2048, first_index=4242, H=H)
+    s = BatchedConvexQPSolver(p, H, max_batch=2048)
+    grf, status, _ = s.solve(rec, con)
+    assert np.all(status == 0), np.bincount(status)
+    viol, swing_nonzero = feasibility_violation(grf, con, p.mu, p.f_max)
+    assert viol <= 1e-9 * p.f_max and not swing_nonzero
+    g2, st2, _ = s.solve(rec[:256], con[:256])
+    assert np.array_equal(g2, grf[:256]) and np.all(st2 == 0)
+    idx = np.random.default_rng(H).choice(2048, 24, replace=False)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec[idx], con[idx], n_threads=8)
+    assert fails == 0
+    assert rel_err(grf[idx], ref) <= TOL_REGRESS
+
+
 def test_a1_params_and_standing_config():
     p, H, rec, con = synth.config_batch(1)
     s = BatchedConvexQPSolver(p, H, max_batch=1)
