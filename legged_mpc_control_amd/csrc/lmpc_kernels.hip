@@ -765,7 +765,6 @@ __device__ __forceinline__ void leg_stage_prep_ipm(const DevParams& prm, const S
     for (int t = 0; t < LS; ++t) {
         if (!valid[t]) continue;
         const int k = lsk[t], j = lsj[t];
-        ldouble* sl = S.st + k * SK;
         gdouble* gl = gs + k * GS;
         const double on = st[t] ? 1.0 : 0.0, off = 1.0 - on;
         const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
@@ -794,7 +793,6 @@ __device__ __forceinline__ void leg_stage_prep(const DevParams& prm, const Smem&
         double du[6] = {0, 0, 0, 0, 0, 0};
         if (valid[t]) {
             const int k = lsk[t], j = lsj[t];
-            ldouble* sl = S.st + k * SK;
             gdouble* gl = gs + k * GS;
             const double R3[9] = {Rt[t][0], Rt[t][1], Rt[t][2], Rt[t][1], Rt[t][3], Rt[t][4], Rt[t][2], Rt[t][4], Rt[t][5]};
             bool fixed[3];
