@@ -163,3 +163,28 @@ def test_third_level_pairs_slacks_as_the_reference_does():
     expect = np.concatenate([t1.f, t0.f]) - np.vstack([t1.d, t0.d]) @ xp + np.concatenate([h0.w_sol, h1.w_sol])
     assert np.allclose(h2.f[nv:nv + npv], expect)
     assert h2.kkt() <= 1e-9
+
+
+def test_wbc_shaped_hierarchy():
+    """The reference WBC's shape (wbc.cpp:93-97): 42 decision variables (18 qdd, 12 forces, 12 torques);
+    level 0 = EOM (18 eq) + torque limits (24 ineq) + friction cone (16 ineq, 4 eq) + no-contact motion;
+    levels 1-2 equalities only, their inequality blocks 0x0 as `matrix_t()` builds them -- so the slack
+    ordering quirk is inert there.  Every level certified by KKT; higher priorities preserved."""
+    rng = np.random.default_rng(21)
+    n = 42
+    a0 = rng.standard_normal((22, n))
+    d0 = rng.standard_normal((40, n))
+    t0 = Q.Task(a0, rng.standard_normal(22), d0, rng.uniform(0.0, 2.0, 40))
+    t1 = Q.Task(rng.standard_normal((12, n)), rng.standard_normal(12), np.zeros((0, 0)), np.zeros(0))
+    t2 = Q.Task(rng.standard_normal((12, n)), rng.standard_normal(12), np.zeros((0, 0)), np.zeros(0))
+    h0 = Q.HoQp(t0)
+    h1 = Q.HoQp(t1, h0)
+    h2 = Q.HoQp(t2, h1)
+    for h in (h0, h1, h2):
+        assert h.kkt() <= 1e-8 * (1 + np.max(np.abs(h.c)))
+    assert h1.num_slack == 0 and h2.num_slack == 0
+    assert np.array_equal(h2.slack_prev, h0.w_sol)  # only level 0 has slacks: aligned with its rows
+    x = h2.solution()
+    assert np.all(t0.d @ x <= t0.f + h0.w_sol + 1e-8)
+    if np.all(h0.w_sol == 0.0):
+        assert np.allclose(t0.a @ x, t0.a @ h0.solution(), atol=1e-6)
