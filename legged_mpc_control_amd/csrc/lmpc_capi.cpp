@@ -38,12 +38,13 @@ struct lmpc_ctx {
     int max_batch = 0;
     lmpc::DevParams prm{};
     hipStream_t stream = nullptr;
-    double* d_rec = nullptr;
-    uint8_t* d_contact = nullptr;
-    double* d_normals = nullptr;  // terrain staging (host _ex path)
-    double* d_grf = nullptr;
-    int32_t* d_status = nullptr;
-    int32_t* d_iters = nullptr;
+    // host-pointer path (lmpc_solve_batch[_ex]): one device block in [rec | normals | contact] and one out
+    // [grf | status | iters], each mirrored by a pinned host block, so a call is one H2D and one D2H copy
+    // (per-tick latency: each separate pageable copy costs its own round of driver staging)
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    uint8_t* h_in = nullptr;
+    uint8_t* h_out = nullptr;
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
     uint8_t* d_done = nullptr;    // per-QP flag: solved by the GI kernel (else the Riccati kernel solves it)
     bool dense_env = false;       // LMPC_DENSE set: it overrides lmpc_set_dense_path
@@ -85,13 +86,17 @@ bool params_ok(const lmpc_params* p) {
     return true;
 }
 
+// staging block sizes of the host-pointer path (bytes)
+size_t in_bytes(int H, int batch) {
+    return (size_t)batch * ((size_t)lmpc_record_len(H) * sizeof(double) + 12 * sizeof(double) + 4 * (size_t)H);
+}
+size_t out_bytes(int H, int batch) { return (size_t)batch * (12 * (size_t)H * sizeof(double) + 2 * sizeof(int32_t)); }
+
 void free_bufs(lmpc_ctx* c) {
-    (void)hipFree(c->d_rec);
-    (void)hipFree(c->d_contact);
-    (void)hipFree(c->d_normals);
-    (void)hipFree(c->d_grf);
-    (void)hipFree(c->d_status);
-    (void)hipFree(c->d_iters);
+    (void)hipFree(c->d_in);
+    (void)hipFree(c->d_out);
+    (void)hipHostFree(c->h_in);
+    (void)hipHostFree(c->h_out);
     (void)hipFree(c->d_scratch);
     (void)hipFree(c->d_done);
     c->d_scratch = nullptr;
@@ -102,12 +107,7 @@ void free_bufs(lmpc_ctx* c) {
     c->d_crec = nullptr;
     c->d_ccon = nullptr;
     c->cmd_qps = 0;
-    c->d_rec = nullptr;
-    c->d_contact = nullptr;
-    c->d_normals = nullptr;
-    c->d_grf = nullptr;
-    c->d_status = nullptr;
-    c->d_iters = nullptr;
+    c->d_in = c->d_out = c->h_in = c->h_out = nullptr;
 }
 
 }  // namespace
@@ -148,13 +148,10 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
         return LMPC_ERR_DEVICE;
     }
     if (max_batch > 0) {
-        const size_t rl = (size_t)lmpc_record_len(horizon);
-        bool ok = hipMalloc(&c->d_rec, (size_t)max_batch * rl * sizeof(double)) == hipSuccess &&
-                  hipMalloc(&c->d_contact, (size_t)max_batch * 4 * horizon) == hipSuccess &&
-                  hipMalloc(&c->d_normals, (size_t)max_batch * 12 * sizeof(double)) == hipSuccess &&
-                  hipMalloc(&c->d_grf, (size_t)max_batch * 12 * horizon * sizeof(double)) == hipSuccess &&
-                  hipMalloc(&c->d_status, (size_t)max_batch * sizeof(int32_t)) == hipSuccess &&
-                  hipMalloc(&c->d_iters, (size_t)max_batch * sizeof(int32_t)) == hipSuccess;
+        const size_t in_b = in_bytes(horizon, max_batch), out_b = out_bytes(horizon, max_batch);
+        bool ok = hipMalloc(&c->d_in, in_b) == hipSuccess && hipMalloc(&c->d_out, out_b) == hipSuccess &&
+                  hipHostMalloc(&c->h_in, in_b, hipHostMallocDefault) == hipSuccess &&
+                  hipHostMalloc(&c->h_out, out_b, hipHostMallocDefault) == hipSuccess;
         if (!ok) {
             free_bufs(c);
             (void)hipStreamDestroy(c->stream);
@@ -265,27 +262,31 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
                 return LMPC_ERR_ARG;
         }
     if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
-    const size_t rl = (size_t)lmpc_record_len(c->H);
     hipStream_t s = c->stream;
-    if (hipMemcpyAsync(c->d_rec, rec, (size_t)batch * rl * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(c->d_contact, contact, (size_t)batch * 4 * c->H, hipMemcpyHostToDevice, s) != hipSuccess)
+    // inputs packed [rec | normals | contact] for THIS batch (offsets from `batch`, so the copy is contiguous)
+    const size_t nrec = (size_t)batch * lmpc_record_len(c->H) * sizeof(double);
+    const size_t nnrm = normals ? (size_t)batch * 12 * sizeof(double) : 0;
+    const size_t ncon = (size_t)batch * 4 * c->H;
+    std::memcpy(c->h_in, rec, nrec);
+    if (normals) std::memcpy(c->h_in + nrec, normals, nnrm);
+    std::memcpy(c->h_in + nrec + nnrm, contact, ncon);
+    if (hipMemcpyAsync(c->d_in, c->h_in, nrec + nnrm + ncon, hipMemcpyHostToDevice, s) != hipSuccess)
         return LMPC_ERR_DEVICE;
-    if (normals && hipMemcpyAsync(c->d_normals, normals, (size_t)batch * 12 * sizeof(double), hipMemcpyHostToDevice,
-                                  s) != hipSuccess)
-        return LMPC_ERR_DEVICE;
-    int rc = lmpc_solve_batch_device_ex(c, c->d_rec, c->d_contact, normals ? c->d_normals : nullptr, batch, c->d_grf,
-                                        c->d_status, c->d_iters, s);
+    const size_t ngrf = (size_t)batch * 12 * c->H * sizeof(double);
+    const size_t nst = (size_t)batch * sizeof(int32_t);
+    double* d_grf = (double*)c->d_out;
+    int32_t* d_st = (int32_t*)(c->d_out + ngrf);
+    int rc = lmpc_solve_batch_device_ex(c, (const double*)c->d_in, c->d_in + nrec + nnrm,
+                                        normals ? (const double*)(c->d_in + nrec) : nullptr, batch, d_grf, d_st,
+                                        d_st + batch, s);
     if (rc != LMPC_OK) return rc;
-    if (hipMemcpyAsync(grf, c->d_grf, (size_t)batch * 12 * c->H * sizeof(double), hipMemcpyDeviceToHost, s) !=
-        hipSuccess)
+    if (hipMemcpyAsync(c->h_out, c->d_out, ngrf + 2 * nst, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
         return LMPC_ERR_DEVICE;
-    if (status && hipMemcpyAsync(status, c->d_status, (size_t)batch * sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
-                      hipSuccess)
-        return LMPC_ERR_DEVICE;
-    if (iters && hipMemcpyAsync(iters, c->d_iters, (size_t)batch * sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
-                     hipSuccess)
-        return LMPC_ERR_DEVICE;
-    return hipStreamSynchronize(s) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
+    std::memcpy(grf, c->h_out, ngrf);
+    if (status) std::memcpy(status, c->h_out + ngrf, nst);
+    if (iters) std::memcpy(iters, c->h_out + ngrf + nst, nst);
+    return LMPC_OK;
 }
 
 int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int batch, double* grf,
