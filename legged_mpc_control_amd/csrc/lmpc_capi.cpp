@@ -90,7 +90,9 @@ bool params_ok(const lmpc_params* p) {
 size_t in_bytes(int H, int batch) {
     return (size_t)batch * ((size_t)lmpc_record_len(H) * sizeof(double) + 12 * sizeof(double) + 4 * (size_t)H);
 }
-size_t out_bytes(int H, int batch) { return (size_t)batch * (12 * (size_t)H * sizeof(double) + 2 * sizeof(int32_t)); }
+size_t out_bytes(int H, int batch) {  // grf | status | iters | dual active-set done flags
+    return (size_t)batch * (12 * (size_t)H * sizeof(double) + 2 * sizeof(int32_t) + 1);
+}
 
 void free_bufs(lmpc_ctx* c) {
     (void)hipFree(c->d_in);
@@ -251,6 +253,8 @@ int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_c
     return lmpc_solve_batch_device_ex(c, d_rec, d_contact, nullptr, batch, d_grf, d_status, d_iters, stream);
 }
 
+static int launch_rc(hipError_t e);
+
 int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, const double* normals, int batch,
                         double* grf, int32_t* status, int32_t* iters) {
     if (!c || batch < 0 || batch > c->max_batch || (batch > 0 && (!rec || !contact || !grf))) return LMPC_ERR_ARG;
@@ -276,13 +280,49 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
     const size_t nst = (size_t)batch * sizeof(int32_t);
     double* d_grf = (double*)c->d_out;
     int32_t* d_st = (int32_t*)(c->d_out + ngrf);
-    int rc = lmpc_solve_batch_device_ex(c, (const double*)c->d_in, c->d_in + nrec + nnrm,
-                                        normals ? (const double*)(c->d_in + nrec) : nullptr, batch, d_grf, d_st,
-                                        d_st + batch, s);
-    if (rc != LMPC_OK) return rc;
-    if (hipMemcpyAsync(c->h_out, c->d_out, ngrf + 2 * nst, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    uint8_t* d_done = c->d_out + ngrf + 2 * nst;  // dual active-set flags travel back with the results
+    const double* d_rec = (const double*)c->d_in;
+    const uint8_t* d_con = c->d_in + nrec + nnrm;
+    const double* d_nrm = normals ? (const double*)(c->d_in + nrec) : nullptr;
+    // The contact schedules are on the host, so this (synchronous) path launches only the kernels the batch
+    // needs: the same routing as lmpc_solve_batch_device_ex, whose QPs skip the other kernel on the device.
+    int n_dense = 0, n_ric = 0;
+    for (int b = 0; b < batch; ++b) {
+        const uint8_t* cb = contact + (size_t)b * 4 * c->H;
+        int n = 0;
+        for (int i = 0; i < 4 * c->H; ++i) n += cb[i] != 0;
+        if (c->prm.dense && n >= 1 && n <= lmpc::DENSE_MAX_LS) ++n_dense;
+        else ++n_ric;
+    }
+    const bool gi = c->prm.dense == 2;
+    if (n_ric && (size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
+    hipError_t e = hipSuccess;
+    if (n_dense)
+        e = gi ? lmpc::launch_gi(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s)
+               : lmpc::launch_dense(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, s);
+    if (e == hipSuccess && n_ric)
+        e = lmpc::launch_qp(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch,
+                            gi ? d_done : nullptr, s);
+    if (e != hipSuccess) return launch_rc(e);
+    const size_t nout = ngrf + 2 * nst + (gi ? (size_t)batch : 0);
+    if (hipMemcpyAsync(c->h_out, c->d_out, nout, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return LMPC_ERR_DEVICE;
+    if (gi && n_dense && !n_ric) {
+        // a QP the dual active set left (step cap, non-finite step) goes to the Riccati kernel, as on the device
+        const uint8_t* hd = c->h_out + ngrf + 2 * nst;
+        bool left = false;
+        for (int b = 0; b < batch && !left; ++b) left = hd[b] == 0;
+        if (left) {
+            if ((size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
+            e = lmpc::launch_qp(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch, d_done,
+                                s);
+            if (e != hipSuccess) return launch_rc(e);
+            if (hipMemcpyAsync(c->h_out, c->d_out, ngrf + 2 * nst, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return LMPC_ERR_DEVICE;
+        }
+    }
     std::memcpy(grf, c->h_out, ngrf);
     if (status) std::memcpy(status, c->h_out + ngrf, nst);
     if (iters) std::memcpy(iters, c->h_out + ngrf + nst, nst);
