@@ -120,6 +120,14 @@ public:
     int last_status() const { return status_; }
     int last_error() const { return error_; }
     int horizon() const { return H_; }
+    // warm start across ticks (the reference's OSQP runs with warm_start = true, ConvexQPSolver.cpp:185):
+    // each tick starts from the previous tick's verified active set, shifted one step (default on)
+    void set_warm_start(bool on) {
+        warm_ = on;
+        have_act_ = false;
+    }
+    bool warm_start() const { return warm_; }
+    int last_iterations() const { return iters_; }  // interior-point iterations | polish rounds << 16
 
 private:
     lmpc_ctx* ctx_ = nullptr;
@@ -128,8 +136,12 @@ private:
     std::vector<double> rec_;
     std::vector<uint8_t> contact_;
     std::vector<double> grf_;
+    std::vector<uint8_t> act_, act_in_;  // last verified active set [H][4]; its one-step shift
+    bool warm_ = true;
+    bool have_act_ = false;
     int status_ = 0;
     int error_ = 0;
+    int iters_ = 0;
 };
 
 }  // namespace legged

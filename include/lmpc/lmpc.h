@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define LMPC_ABI_VERSION 3 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection */
+#define LMPC_ABI_VERSION 4 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
+                              4: warm start (lmpc_solve_batch_warm, lmpc_shift_active_set) */
 #define LMPC_MAX_HORIZON 32
 
 /* return codes (API level) */
@@ -159,6 +160,21 @@ void lmpc_terrain_frame(const double normal[3], double R[9] /* row-major */);
 int lmpc_solve_batch_ex(lmpc_ctx* ctx, const double* rec, const uint8_t* contact,
                         const double* normals, int batch, double* grf, int32_t* status,
                         int32_t* iters);
+/* Warm start across MPC ticks (the reference's OSQP runs with warm_start = true,
+ * ConvexQPSolver.cpp:185).  act_in / act_out: [batch][H][4] u8 per leg-step (layout of
+ * `contact`): bits 0-3 the active pyramid faces (+fx, -fx, +fy, -fy rows of QPS:131-158),
+ * bit 4 the f_max bound, 15 a lift-off leg (f = 0).  The Riccati kernel starts each QP in
+ * its active-set polish from act_in (NULL: cold), which verifies the KKT conditions; a set
+ * that does not verify within 12 polish rounds falls back to the cold interior point, so the
+ * answer is the same exact optimum either way.  act_out (may be NULL) receives the verified
+ * set, 0 for swing legs.  Every QP of a warm call runs on the Riccati kernel (the condensed
+ * dense kernels are not warm-started).  Host buffers, synchronous. */
+int lmpc_solve_batch_warm(lmpc_ctx* ctx, const double* rec, const uint8_t* contact,
+                          const double* normals, int batch, const uint8_t* act_in,
+                          uint8_t* act_out, double* grf, int32_t* status, int32_t* iters);
+/* One MPC step later: stage k takes stage k+1's set, the last stage keeps its own
+ * (shifted may alias act). */
+void lmpc_shift_active_set(const uint8_t* act, int batch, int H, uint8_t* shifted);
 /* device buffers, asynchronous (normals unchecked: the caller guarantees n_z > 0) */
 int lmpc_solve_batch_device_ex(lmpc_ctx* ctx, const double* d_rec, const uint8_t* d_contact,
                                const double* d_normals, int batch, double* d_grf,

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "lmpc_predict_contact", "lmpc_current_contact", "lmpc_contact_schedule", "lmpc_pack_record",
     "lmpc_synth_cfg_go1", "lmpc_synth_cfg_a1_standing", "lmpc_synth_fill",
     # ABI 2: terrain extension
-    "lmpc_terrain_frame", "lmpc_solve_batch_ex", "lmpc_solve_batch_device_ex", "lmpc_synth_normals",
+    "lmpc_terrain_frame", "lmpc_solve_batch_ex", "lmpc_solve_batch_warm", "lmpc_shift_active_set", "lmpc_solve_batch_device_ex", "lmpc_synth_normals",
     # on-device input generation
     "lmpc_command_to_record", "lmpc_build_records_device", "lmpc_solve_commands_device",
     "lmpc_synth_commands", "lmpc_synth_commands_device", "lmpc_synth_normals_device",
@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     # ABI 3: dense-path selection
     "lmpc_set_dense_path", "lmpc_get_dense_path",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class LmpcParams(ctypes.Structure):
@@ -174,6 +174,10 @@ def lib():
         L.lmpc_terrain_frame.restype = None
         L.lmpc_solve_batch_ex.argtypes = [vp, dp, u8p, dp, ctypes.c_int, dp, i32p, i32p]
         L.lmpc_solve_batch_ex.restype = ctypes.c_int
+        L.lmpc_solve_batch_warm.argtypes = [vp, dp, u8p, dp, ctypes.c_int, u8p, u8p, dp, i32p, i32p]
+        L.lmpc_solve_batch_warm.restype = ctypes.c_int
+        L.lmpc_shift_active_set.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
+        L.lmpc_shift_active_set.restype = None
         L.lmpc_solve_batch_device_ex.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
         L.lmpc_solve_batch_device_ex.restype = ctypes.c_int
         L.lmpc_synth_normals.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_double, dp]

@@ -20,6 +20,8 @@ ConvexQPSolver::ConvexQPSolver(const double* q_weights, const double* r_weights,
     rec_.assign((size_t)lmpc_record_len(H_), 0.0);
     contact_.assign((size_t)4 * H_, 1);
     grf_.assign((size_t)12 * H_, 0.0);
+    act_.assign((size_t)4 * H_, 0);
+    act_in_.assign((size_t)4 * H_, 0);
     error_ = lmpc_create(&params_, H_, 1, device, &ctx_);
     // one QP per call: the dual active set has the lower latency (no batch tail to wait for)
     if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_GI);
@@ -39,8 +41,13 @@ ConvexQPSolver& ConvexQPSolver::operator=(ConvexQPSolver&& o) noexcept {
         rec_ = std::move(o.rec_);
         contact_ = std::move(o.contact_);
         grf_ = std::move(o.grf_);
+        act_ = std::move(o.act_);
+        act_in_ = std::move(o.act_in_);
+        warm_ = o.warm_;
+        have_act_ = o.have_act_;
         status_ = o.status_;
         error_ = o.error_;
+        iters_ = o.iters_;
     }
     return *this;
 }
@@ -68,9 +75,24 @@ void ConvexQPSolver::calc_mpc_reference(LeggedState& state, LeggedContactFSM leg
 // ConvexQPSolver::compute_grfs (ConvexQPSolver.cpp:314-327): returns u_0; NaN -> zeros
 std::array<double, DIM_GRF> ConvexQPSolver::compute_grfs(LeggedState& /*state*/) {
     std::array<double, DIM_GRF> out{};
-    int32_t st = 0;
-    error_ = ctx_ ? lmpc_solve_batch(ctx_, rec_.data(), contact_.data(), 1, grf_.data(), &st, nullptr) : LMPC_ERR_DEVICE;
+    int32_t st = 0, it = 0;
+    if (!ctx_) {
+        error_ = LMPC_ERR_DEVICE;
+    } else if (warm_ && have_act_) {
+        // previous tick's verified set, one step on; a set that no longer verifies falls back to the cold
+        // interior point inside the kernel, so the answer is the exact optimum either way
+        lmpc_shift_active_set(act_.data(), 1, H_, act_in_.data());
+        error_ = lmpc_solve_batch_warm(ctx_, rec_.data(), contact_.data(), nullptr, 1, act_in_.data(), act_.data(),
+                                       grf_.data(), &st, &it);
+    } else if (warm_) {
+        error_ = lmpc_solve_batch_warm(ctx_, rec_.data(), contact_.data(), nullptr, 1, nullptr, act_.data(),
+                                       grf_.data(), &st, &it);
+    } else {
+        error_ = lmpc_solve_batch(ctx_, rec_.data(), contact_.data(), 1, grf_.data(), &st, &it);
+    }
+    have_act_ = warm_ && error_ == LMPC_OK && st == LMPC_QP_CONVERGED;
     status_ = st;
+    iters_ = it;
     if (error_ != LMPC_OK) return out;  // zeros, as the reference returns on a failed solve
     for (int i = 0; i < DIM_GRF; ++i) out[i] = grf_[i];
     return out;

@@ -87,11 +87,11 @@ bool params_ok(const lmpc_params* p) {
 }
 
 // staging block sizes of the host-pointer path (bytes)
-size_t in_bytes(int H, int batch) {
-    return (size_t)batch * ((size_t)lmpc_record_len(H) * sizeof(double) + 12 * sizeof(double) + 4 * (size_t)H);
+size_t in_bytes(int H, int batch) {  // rec | normals | contact | warm-start active set
+    return (size_t)batch * ((size_t)lmpc_record_len(H) * sizeof(double) + 12 * sizeof(double) + 8 * (size_t)H);
 }
-size_t out_bytes(int H, int batch) {  // grf | status | iters | dual active-set done flags
-    return (size_t)batch * (12 * (size_t)H * sizeof(double) + 2 * sizeof(int32_t) + 1);
+size_t out_bytes(int H, int batch) {  // grf | status | iters | dual active-set done flags | active set out
+    return (size_t)batch * (12 * (size_t)H * sizeof(double) + 2 * sizeof(int32_t) + 1 + 4 * (size_t)H);
 }
 
 void free_bufs(lmpc_ctx* c) {
@@ -142,6 +142,8 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     {
         const char* gm = std::getenv("LMPC_GI_MAX_STEPS");  // test hook: exercise the hand-over to the Riccati kernel
         c->prm.gi_max_steps = gm ? std::atoi(gm) : 240;
+        const char* wr = std::getenv("LMPC_WARM_ROUNDS");  // tuning hook (tools/)
+        c->prm.warm_rounds = wr ? std::atoi(wr) : 12;  // tools/tick_latency sweep: 4 -> 0.59 ms, 12 -> 0.35 ms at H=30
     }
     if (hipDeviceGetAttribute(&c->prm.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         c->prm.cus = 256;
@@ -255,8 +257,10 @@ int lmpc_solve_batch_device(lmpc_ctx* c, const double* d_rec, const uint8_t* d_c
 
 static int launch_rc(hipError_t e);
 
-int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, const double* normals, int batch,
-                        double* grf, int32_t* status, int32_t* iters) {
+// The host-pointer path: one pinned copy in, the kernels, one pinned copy out.  act_in / act_out (warm start,
+// lmpc_solve_batch_warm): every QP goes to the Riccati kernel, which starts from act_in and reports act_out.
+static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, const double* normals, int batch,
+                      const uint8_t* act_in, uint8_t* act_out, double* grf, int32_t* status, int32_t* iters) {
     if (!c || batch < 0 || batch > c->max_batch || (batch > 0 && (!rec || !contact || !grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
     if (normals)
@@ -267,23 +271,31 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
         }
     if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
     hipStream_t s = c->stream;
-    // inputs packed [rec | normals | contact] for THIS batch (offsets from `batch`, so the copy is contiguous)
+    const bool warm = act_in || act_out;
+    lmpc::DevParams prm = c->prm;
+    if (warm) prm.dense = 0;  // the dense kernels are not warm-started
+    // inputs packed [rec | normals | contact | act_in] for THIS batch (offsets from `batch`: one contiguous copy)
     const size_t nrec = (size_t)batch * lmpc_record_len(c->H) * sizeof(double);
     const size_t nnrm = normals ? (size_t)batch * 12 * sizeof(double) : 0;
     const size_t ncon = (size_t)batch * 4 * c->H;
+    const size_t nact = act_in ? ncon : 0;
     std::memcpy(c->h_in, rec, nrec);
     if (normals) std::memcpy(c->h_in + nrec, normals, nnrm);
     std::memcpy(c->h_in + nrec + nnrm, contact, ncon);
-    if (hipMemcpyAsync(c->d_in, c->h_in, nrec + nnrm + ncon, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (act_in) std::memcpy(c->h_in + nrec + nnrm + ncon, act_in, nact);
+    if (hipMemcpyAsync(c->d_in, c->h_in, nrec + nnrm + ncon + nact, hipMemcpyHostToDevice, s) != hipSuccess)
         return LMPC_ERR_DEVICE;
     const size_t ngrf = (size_t)batch * 12 * c->H * sizeof(double);
     const size_t nst = (size_t)batch * sizeof(int32_t);
     double* d_grf = (double*)c->d_out;
     int32_t* d_st = (int32_t*)(c->d_out + ngrf);
     uint8_t* d_done = c->d_out + ngrf + 2 * nst;  // dual active-set flags travel back with the results
+    uint8_t* d_aout = d_done + batch;
     const double* d_rec = (const double*)c->d_in;
     const uint8_t* d_con = c->d_in + nrec + nnrm;
     const double* d_nrm = normals ? (const double*)(c->d_in + nrec) : nullptr;
+    prm.warm_act = act_in ? c->d_in + nrec + nnrm + ncon : nullptr;
+    prm.act_out = act_out ? d_aout : nullptr;
     // The contact schedules are on the host, so this (synchronous) path launches only the kernels the batch
     // needs: the same routing as lmpc_solve_batch_device_ex, whose QPs skip the other kernel on the device.
     int n_dense = 0, n_ric = 0;
@@ -291,20 +303,21 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
         const uint8_t* cb = contact + (size_t)b * 4 * c->H;
         int n = 0;
         for (int i = 0; i < 4 * c->H; ++i) n += cb[i] != 0;
-        if (c->prm.dense && n >= 1 && n <= lmpc::DENSE_MAX_LS) ++n_dense;
+        if (prm.dense && n >= 1 && n <= lmpc::DENSE_MAX_LS) ++n_dense;
         else ++n_ric;
     }
-    const bool gi = c->prm.dense == 2;
+    const bool gi = prm.dense == 2;
     if (n_ric && (size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
     hipError_t e = hipSuccess;
     if (n_dense)
-        e = gi ? lmpc::launch_gi(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s)
-               : lmpc::launch_dense(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, s);
+        e = gi ? lmpc::launch_gi(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s)
+               : lmpc::launch_dense(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, s);
     if (e == hipSuccess && n_ric)
-        e = lmpc::launch_qp(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch,
+        e = lmpc::launch_qp(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch,
                             gi ? d_done : nullptr, s);
     if (e != hipSuccess) return launch_rc(e);
-    const size_t nout = ngrf + 2 * nst + (gi ? (size_t)batch : 0);
+    // one copy back: [grf | status | iters], plus the done flags (dual active set) or the active set (warm)
+    const size_t nout = act_out ? ngrf + 2 * nst + batch + ncon : ngrf + 2 * nst + (gi ? (size_t)batch : 0);
     if (hipMemcpyAsync(c->h_out, c->d_out, nout, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return LMPC_ERR_DEVICE;
@@ -315,8 +328,7 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
         for (int b = 0; b < batch && !left; ++b) left = hd[b] == 0;
         if (left) {
             if ((size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
-            e = lmpc::launch_qp(c->prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch, d_done,
-                                s);
+            e = lmpc::launch_qp(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch, d_done, s);
             if (e != hipSuccess) return launch_rc(e);
             if (hipMemcpyAsync(c->h_out, c->d_out, ngrf + 2 * nst, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
@@ -326,7 +338,28 @@ int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, 
     std::memcpy(grf, c->h_out, ngrf);
     if (status) std::memcpy(status, c->h_out + ngrf, nst);
     if (iters) std::memcpy(iters, c->h_out + ngrf + nst, nst);
+    if (act_out) std::memcpy(act_out, c->h_out + ngrf + 2 * nst + batch, ncon);
     return LMPC_OK;
+}
+
+int lmpc_solve_batch_ex(lmpc_ctx* c, const double* rec, const uint8_t* contact, const double* normals, int batch,
+                        double* grf, int32_t* status, int32_t* iters) {
+    return solve_host(c, rec, contact, normals, batch, nullptr, nullptr, grf, status, iters);
+}
+
+int lmpc_solve_batch_warm(lmpc_ctx* c, const double* rec, const uint8_t* contact, const double* normals, int batch,
+                          const uint8_t* act_in, uint8_t* act_out, double* grf, int32_t* status, int32_t* iters) {
+    return solve_host(c, rec, contact, normals, batch, act_in, act_out, grf, status, iters);
+}
+
+void lmpc_shift_active_set(const uint8_t* act, int batch, int H, uint8_t* shifted) {
+    if (!act || !shifted || batch <= 0 || H <= 0) return;
+    for (int b = 0; b < batch; ++b) {
+        const uint8_t* a = act + (size_t)b * 4 * H;
+        uint8_t* o = shifted + (size_t)b * 4 * H;
+        for (int k = 0; k < H; ++k)
+            for (int j = 0; j < 4; ++j) o[4 * k + j] = a[4 * (k + 1 < H ? k + 1 : k) + j];
+    }
 }
 
 int lmpc_solve_batch(lmpc_ctx* c, const double* rec, const uint8_t* contact, int batch, double* grf,

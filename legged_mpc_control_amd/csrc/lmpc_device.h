@@ -26,6 +26,13 @@ struct DevParams {
                        // point (lmpc_dense.hip), 2 condensed dual active set (lmpc_gi.hip)
     int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel
     int cus;           // compute units of the device (launch shaping only)
+    // warm start of the Riccati kernel (per QP and leg-step [B][H][4]: bits 0-4 = active pyramid faces and
+    // bound, 15 = lift-off apex).  warm_act != nullptr: the kernel starts in the active-set polish from it and
+    // falls back to the cold interior point if the polish does not verify within max_rounds; act_out receives
+    // the verified active set.  Both null by default.
+    const uint8_t* warm_act;
+    uint8_t* act_out;
+    int warm_rounds;   // polish rounds a warm start may take before the cold fallback
 };
 constexpr int DENSE_MAX_LS = 20;  // 5 leg-steps per 16-wide tile x 4 tiles (lmpc_dense.hip)
 constexpr int DENSE_MAX_H = 16;   // the dense path's per-step LDS arrays

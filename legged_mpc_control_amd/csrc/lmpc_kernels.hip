@@ -1062,6 +1062,9 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
     int qstatus = LMPC_QP_CONVERGED;
     int ipm_it = 0, prounds = 0;
     bool done = false;
+    int act_fin[LS];  // verified active set (warm-start output); 0 = none / unconstrained
+#pragma unroll
+    for (int t = 0; t < LS; ++t) act_fin[t] = 0;
     if (nst > 0.5) {
         // One loop, three modes, so that factor / solve / adjoint are each
         // instantiated once (keeps the code object small for the I-cache).
@@ -1072,6 +1075,16 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
         int mode = PRED;
         int act[LS];
         bool apex[LS];
+        // warm start: straight into the polish from the given active set (the caller's previous solution)
+        bool warm = prm.warm_act != nullptr;
+        if (warm) {
+#pragma unroll
+            for (int t = 0; t < LS; ++t) {
+                const int ls = lane + 64 * t;
+                act[t] = st[t] ? (prm.warm_act[(size_t)qp * 4 * H + ls] & 31) : 0;
+            }
+            mode = POLISH;
+        }
         double ua[LS][3];  // predictor step u_aff: the only predictor state kept across the corrector solve
 #pragma unroll
         for (int t = 0; t < LS; ++t) ua[t][0] = ua[t][1] = ua[t][2] = 0.0;
@@ -1332,9 +1345,17 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                 }
                 if (!__any(changed)) {
                     done = true;
+#pragma unroll
+                    for (int t = 0; t < LS; ++t) act_fin[t] = st[t] ? act[t] : 0;
                     break;
                 }
-                if (++rd >= prm.max_rounds) {
+                if (++rd >= (warm ? prm.warm_rounds : prm.max_rounds)) {
+                    if (warm) {  // the warm active set did not verify: the cold interior point
+                        warm = false;
+                        rd = 0;
+                        mode = PRED;
+                        continue;
+                    }
                     // retry: tighter interior point, then a fresh polish
                     if (++att >= prm.max_attempts) break;
                     tol *= 1e-3;
@@ -1379,6 +1400,11 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
     }
     STAMP(5);  // epilogue
     STAMP_FLUSH(qp);
+    if (prm.act_out) {
+#pragma unroll
+        for (int t = 0; t < LS; ++t)
+            if (valid[t]) prm.act_out[(size_t)qp * 4 * H + lane + 64 * t] = (uint8_t)(anybad ? 0 : act_fin[t]);
+    }
     if (lane == 0) {
         if (status) status[qp] = anybad ? LMPC_QP_NAN : qstatus;
         if (iters) iters[qp] = ipm_it | (prounds << 16);

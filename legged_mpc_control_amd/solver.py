@@ -113,6 +113,48 @@ class BatchedConvexQPSolver:
                                             iters.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "lmpc_solve_batch_ex")
         return grf, status, iters
 
+    def solve_warm(self, rec: np.ndarray, contact: np.ndarray, act_in: np.ndarray | None = None,
+                   normals: np.ndarray | None = None):
+        """Warm-started solve (lmpc_solve_batch_warm): act_in [B,H,4] u8 active sets (None = cold) ->
+        (grf, status, iters, act_out [B,H,4]).  Every QP runs on the Riccati kernel's active-set polish
+        from act_in, falling back to its cold interior point; the optimum is the same either way."""
+        rec = np.ascontiguousarray(rec, dtype=np.float64)
+        contact = np.ascontiguousarray(contact, dtype=np.uint8)
+        B = rec.shape[0]
+        if rec.shape != (B, self.record_len) or contact.shape != (B, self.H, 4):
+            raise ValueError("bad record/contact shape")
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        aptr = None
+        if act_in is not None:
+            act_in = np.ascontiguousarray(act_in, dtype=np.uint8)
+            if act_in.shape != (B, self.H, 4):
+                raise ValueError("act_in must be [B, H, 4]")
+            aptr = act_in.ctypes.data_as(u8)
+        nptr = None
+        if normals is not None:
+            normals = np.ascontiguousarray(normals, dtype=np.float64)
+            if normals.shape != (B, 4, 3):
+                raise ValueError("normals must be [B, 4, 3]")
+            nptr = _dp(normals)
+        grf = np.zeros((B, self.H, 12), dtype=np.float64)
+        status = np.zeros(B, dtype=np.int32)
+        iters = np.zeros(B, dtype=np.int32)
+        act_out = np.zeros((B, self.H, 4), dtype=np.uint8)
+        i32 = ctypes.POINTER(ctypes.c_int32)
+        N.check(self._L.lmpc_solve_batch_warm(self._ctx, _dp(rec), contact.ctypes.data_as(u8), nptr, B, aptr,
+                                              act_out.ctypes.data_as(u8), _dp(grf), status.ctypes.data_as(i32),
+                                              iters.ctypes.data_as(i32)), "lmpc_solve_batch_warm")
+        return grf, status, iters, act_out
+
+    @staticmethod
+    def shift_active_set(act: np.ndarray) -> np.ndarray:
+        """One MPC step later (lmpc_shift_active_set): stage k <- k+1, the last stage keeps its own."""
+        act = np.ascontiguousarray(act, dtype=np.uint8)
+        out = np.empty_like(act)
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        N.lib().lmpc_shift_active_set(act.ctypes.data_as(u8), act.shape[0], act.shape[1], out.ctypes.data_as(u8))
+        return out
+
     def solve_device(self, rec, contact, grf, status=None, iters=None, stream=None, normals=None) -> None:
         """Device tensors (torch, resident in HBM) in/out; asynchronous on `stream`
         (a torch.cuda.Stream or raw hipStream_t int; default = torch's current stream).

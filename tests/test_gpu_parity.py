@@ -469,3 +469,34 @@ def test_gi_step_cap_hands_over_to_riccati(monkeypatch):
     assert np.all((it[handed] >> 16) >= 1)        # Riccati: polish rounds in the high bits
     assert np.array_equal(it[~handed], it2[~handed])
     assert rel_err(g, ref) <= TOL_REGRESS and rel_err(g2, ref) <= TOL_REGRESS
+
+
+@pytest.mark.parametrize("cid", [5, 2])
+def test_warm_start(cid):
+    """lmpc_solve_batch_warm: the polish from a verified set re-verifies in one round with no interior-point
+    iteration and the same answer; from a neighbouring QP's set (perturbed state) it reaches the perturbed QP's
+    optimum in fewer iterations than cold; from arbitrary bytes it falls back to the cold interior point."""
+    p, H, rec, con = synth.config_batch(cid, count=64, first_index=777)
+    s = BatchedConvexQPSolver(p, H, max_batch=64)
+    op = O.params_from(p)
+    g0, st0, it0, a0 = s.solve_warm(rec, con)  # cold, on the Riccati kernel
+    ref, _, fails = O.solve_batch(op, H, rec, con, n_threads=8)
+    assert fails == 0 and np.all(st0 == 0) and rel_err(g0, ref) <= TOL_REGRESS
+    assert np.all(a0[con == 0] == 0)
+    g1, st1, it1, a1 = s.solve_warm(rec, con, act_in=a0)
+    assert np.all(st1 == 0) and np.all((it1 & 0xFFFF) == 0) and np.all((it1 >> 16) == 1)
+    assert np.array_equal(a1, a0) and rel_err(g1, g0) <= 1e-12
+    rec2 = rec.copy()
+    rec2[:, 6:12] += np.random.default_rng(cid).normal(0.0, 0.02, (64, 6))  # angular / linear velocity
+    ref2, _, fails = O.solve_batch(op, H, rec2, con, n_threads=8)
+    gw, stw, itw, _ = s.solve_warm(rec2, con, act_in=a0)
+    gc, stc, itc, _ = s.solve_warm(rec2, con)
+    assert fails == 0 and np.all(stw == 0) and np.all(stc == 0)
+    assert rel_err(gw, ref2) <= TOL_REGRESS and rel_err(gc, ref2) <= TOL_REGRESS
+    work = lambda it: 2 * (it & 0xFFFF) + (it >> 16)  # solves per QP
+    assert work(itw).mean() < 0.5 * work(itc).mean()
+    junk = np.random.default_rng(1).integers(0, 256, a0.shape).astype(np.uint8)
+    gj, stj, _, _ = s.solve_warm(rec, con, act_in=junk)
+    assert np.all(stj == 0) and rel_err(gj, ref) <= TOL_REGRESS
+    sh = BatchedConvexQPSolver.shift_active_set(a0)
+    assert np.array_equal(sh[:, :-1], a0[:, 1:]) and np.array_equal(sh[:, -1], a0[:, -1])

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "lmpc/ConvexQPSolver.hpp"
@@ -15,6 +16,7 @@ using namespace legged;
 int main(int argc, char** argv) {
     const int H = argc > 1 ? std::atoi(argv[1]) : 10;
     const int ticks = argc > 2 ? std::atoi(argv[2]) : 2000;
+    const bool warm = !(argc > 3 && std::string(argv[3]) == "cold");  // default: warm start across ticks
     LeggedState state;
     const double q[12] = {50.0, 100.0, 0.0, 0.0, 0.0, 3500.0, 0.01, 0.01, 10.0, 15.0, 15.0, 20.0};  // Go1 sim
     for (int i = 0; i < 12; ++i) {
@@ -33,7 +35,9 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "create failed: %s\n", lmpc_strerror(fastConvex.last_error()));
         return 2;
     }
+    fastConvex.set_warm_start(warm);
     std::vector<double> ms;
+    double solves = 0.0;
     int bad = 0;
     for (int tick = 0; tick < ticks + 50; ++tick) {
         for (int i = 0; i < NUM_LEG; ++i) {
@@ -53,14 +57,19 @@ int main(int argc, char** argv) {
         std::array<double, DIM_GRF> u0 = fastConvex.compute_grfs(state);
         const auto t1 = std::chrono::steady_clock::now();
         bad += fastConvex.last_error() != LMPC_OK || fastConvex.last_status() != 0 || !std::isfinite(u0[2]);
-        if (tick >= 50) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+        if (tick >= 50) {
+            ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            const int it = fastConvex.last_iterations();
+            solves += 2 * (it & 0xFFFF) + (it >> 16);  // Riccati solves (cold dual active set: 0 + steps)
+        }
     }
     std::sort(ms.begin(), ms.end());
     double mean = 0.0;
     for (double v : ms) mean += v;
     mean /= ms.size();
-    std::printf("{\"horizon\": %d, \"ticks\": %zu, \"mean_ms\": %.4f, \"median_ms\": %.4f, \"p99_ms\": %.4f, "
-                "\"max_ms\": %.4f, \"failed_ticks\": %d}\n",
-                H, ms.size(), mean, ms[ms.size() / 2], ms[(size_t)(0.99 * ms.size())], ms.back(), bad);
+    std::printf("{\"horizon\": %d, \"warm_start\": %s, \"ticks\": %zu, \"mean_ms\": %.4f, \"median_ms\": %.4f, "
+                "\"p99_ms\": %.4f, \"max_ms\": %.4f, \"failed_ticks\": %d, \"mean_riccati_solves\": %.2f}\n",
+                H, warm ? "true" : "false", ms.size(), mean, ms[ms.size() / 2], ms[(size_t)(0.99 * ms.size())],
+                ms.back(), bad, solves / ms.size());
     return bad ? 3 : 0;
 }
