@@ -63,13 +63,22 @@ def main():
     rank, world, local_rank = D.env_rank()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # one GPU per rank on a node (LOCAL_RANK < device count); the modulo only matters when rehearsing
+    # several ranks on fewer GPUs (a 1-GPU box), where it never changes what a rank computes
+    local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL (the product path); LMPC_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU, which RCCL
+        # refuses ("duplicate GPU")
+        backend = os.environ.get("LMPC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     cfg = synth.CONFIGS[args.config]
     H = cfg["H"]
@@ -201,7 +210,7 @@ def main():
         tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
         wl = wl_name if args.batch is None else None
         if wl in tr:
-            traffic_bytes = tr[wl]["bytes_per_launch"]
+            traffic_bytes = tr[wl]["bytes_per_qp"] * B  # this rank's launch (config 4 at N > 1: 65536/N QPs)
     except (OSError, ValueError, KeyError):
         traffic_bytes = None
 
