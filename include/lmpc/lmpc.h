@@ -22,6 +22,13 @@
  * All arithmetic is fp64, as in the reference (Eigen double).  Plain C types
  * only; no exceptions cross this boundary.  A context is NOT thread-safe
  * (like the reference solver object): use one context per host thread.
+ * Every entry point runs on the context's device and restores the caller's
+ * current HIP device before it returns; a stream passed in must belong to the
+ * context's device (LMPC_ERR_ARG otherwise).  Calls on one context are
+ * ordered as issued even when they use different streams (the context's
+ * factor workspace, hand-over flags and staging blocks are shared by every
+ * entry point): an asynchronous device-path call on stream A followed by a
+ * call on stream B or a host-pointer call makes B / the host wait for A.
  *
  * Per-instance record layout (doubles, see lmpc_record_len):
  *   [ x0(12) | rot(9, row-major body->world) | feet(4 legs x xyz, world-aligned,
@@ -115,7 +122,9 @@ int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
  * LMPC_DENSE_IPM (interior point + active-set polish; the default: fastest when every SIMD holds one QP
  * and the launch waits for its slowest, e.g. 1024 QPs) or LMPC_DENSE_GI (dual active set: about half
  * the mean cost per QP, a longer tail -- the choice for one QP per call, e.g. the per-tick drop-in);
- * LMPC_DENSE_OFF sends every QP to the Riccati kernel.  All return the same optimum.  Set it before
+ * LMPC_DENSE_OFF sends every QP to the Riccati kernel.  All return the same optimum: a dense QP left
+ * without a verified optimum (iteration or step cap, non-finite iterate) is solved by the Riccati
+ * kernel in the same call, so its status is the Riccati kernel's.  Set it before
  * solving; the environment variable LMPC_DENSE (0 / ipm / gi), when set, overrides this call.
  * lmpc_get_dense_path returns the path in effect (LMPC_DENSE_OFF when H > 16). */
 #define LMPC_DENSE_OFF 0
@@ -142,7 +151,8 @@ int lmpc_solve_batch_device(lmpc_ctx* ctx, const double* d_rec, const uint8_t* d
                             int batch, double* d_grf, int32_t* d_status, int32_t* d_iters,
                             void* stream);
 
-/* Synchronise the context's stream. */
+/* Wait for everything the context has issued: its own stream and the last
+ * device-path launch on a caller's stream. */
 int lmpc_sync(lmpc_ctx* ctx);
 
 /* ---- terrain extension (ABI 2) -------------

@@ -23,7 +23,10 @@ ConvexQPSolver::ConvexQPSolver(const double* q_weights, const double* r_weights,
     act_.assign((size_t)4 * H_, 0);
     act_in_.assign((size_t)4 * H_, 0);
     error_ = lmpc_create(&params_, H_, 1, device, &ctx_);
-    // one QP per call: the dual active set has the lower latency (no batch tail to wait for)
+    // Warm start is on by default (set_warm_start): every tick then runs on the Riccati kernel, from the
+    // previous tick's verified active set (the first tick from the cold interior point).  Cold solves
+    // (set_warm_start(false)) take the dual active set, the lower-latency dense kernel for one QP per call.
+    // The Python drop-in (legged_mpc_control_amd.ConvexQPSolver) has the same defaults.
     if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_GI);
 }
 

@@ -21,7 +21,7 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
 hipError_t launch_gi(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                      int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
 hipError_t launch_dense(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
-                        int batch, double* grf, int32_t* status, int32_t* iters, hipStream_t stream);
+                        int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
 hipError_t launch_records(const lmpc_command* cmd, int batch, int H, double dt, double* rec, uint8_t* contact,
                           hipStream_t stream);
 hipError_t launch_synth(const lmpc_synth_cfg& cfg, uint64_t seed, int64_t first, int count, lmpc_command* cmd,
@@ -46,12 +46,18 @@ struct lmpc_ctx {
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
-    uint8_t* d_done = nullptr;    // per-QP flag: solved by the GI kernel (else the Riccati kernel solves it)
+    uint8_t* d_done = nullptr;    // per-QP flag: solved by the dense-path kernel (else the Riccati kernel solves it)
     bool dense_env = false;       // LMPC_DENSE set: it overrides lmpc_set_dense_path
     size_t scratch_qps = 0;
     double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
     uint8_t* d_ccon = nullptr;
     size_t cmd_qps = 0;
+    // Ordering of the context's own buffers (d_scratch, d_done, the staging blocks, d_crec/d_ccon) across
+    // streams: recorded after every launch that uses them, waited on by the next such launch when it comes on
+    // another stream (ctx_enter / ctx_leave).
+    hipEvent_t ev = nullptr;
+    hipStream_t ev_stream = nullptr;
+    bool ev_live = false;
 };
 
 namespace {
@@ -90,8 +96,48 @@ bool params_ok(const lmpc_params* p) {
 size_t in_bytes(int H, int batch) {  // rec | normals | contact | warm-start active set
     return (size_t)batch * ((size_t)lmpc_record_len(H) * sizeof(double) + 12 * sizeof(double) + 8 * (size_t)H);
 }
-size_t out_bytes(int H, int batch) {  // grf | status | iters | dual active-set done flags | active set out
+size_t out_bytes(int H, int batch) {  // grf | status | iters | dense-path hand-over flags | active set out
     return (size_t)batch * (12 * (size_t)H * sizeof(double) + 2 * sizeof(int32_t) + 1 + 4 * (size_t)H);
+}
+
+// Every entry point runs on the context's device and leaves the caller's current device as it found it.
+struct DeviceScope {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            prev = -1;
+            return;
+        }
+        ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+// A caller's stream must belong to the context's device (the null stream is the current device's, which
+// DeviceScope has just made the context's).
+bool stream_ok(hipStream_t s, int dev) {
+    if (!s) return true;
+    hipDevice_t d = -1;
+    return hipStreamGetDevice(s, &d) == hipSuccess && d == dev;
+}
+
+// Launches that use the context's buffers are ordered as issued, whatever stream each comes on: before one,
+// the stream waits for the event recorded after the previous one (when that ran on another stream); after
+// it, the event is recorded again.  Device-path calls on a single stream pay one event record each.
+hipError_t ctx_enter(lmpc_ctx* c, hipStream_t s) {
+    if (c->ev_live && c->ev_stream != s) return hipStreamWaitEvent(s, c->ev, 0);
+    return hipSuccess;
+}
+hipError_t ctx_leave(lmpc_ctx* c, hipStream_t s) {
+    const hipError_t e = hipEventRecord(c->ev, s);
+    c->ev_stream = s;
+    c->ev_live = e == hipSuccess;
+    return e;
 }
 
 void free_bufs(lmpc_ctx* c) {
@@ -121,7 +167,8 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LMPC_ERR_DEVICE;
-    if (hipSetDevice(device) != hipSuccess) return LMPC_ERR_DEVICE;
+    DeviceScope ds(device);
+    if (!ds.ok) return LMPC_ERR_DEVICE;
     lmpc_ctx* c = new (std::nothrow) lmpc_ctx();
     if (!c) return LMPC_ERR_ALLOC;
     c->device = device;
@@ -142,12 +189,19 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     {
         const char* gm = std::getenv("LMPC_GI_MAX_STEPS");  // test hook: exercise the hand-over to the Riccati kernel
         c->prm.gi_max_steps = gm ? std::atoi(gm) : 240;
+        const char* dc = std::getenv("LMPC_DENSE_ITER_CAP");  // test hook: the interior point's hand-over
+        c->prm.dense_iter_cap = dc ? std::atoi(dc) : (1 << 30);
         const char* wr = std::getenv("LMPC_WARM_ROUNDS");  // tuning hook (tools/)
         c->prm.warm_rounds = wr ? std::atoi(wr) : 12;  // tools/tick_latency sweep: 4 -> 0.59 ms, 12 -> 0.35 ms at H=30
     }
     if (hipDeviceGetAttribute(&c->prm.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         c->prm.cus = 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return LMPC_ERR_DEVICE;
+    }
+    if (hipEventCreateWithFlags(&c->ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
         delete c;
         return LMPC_ERR_DEVICE;
     }
@@ -158,6 +212,7 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
                   hipHostMalloc(&c->h_out, out_b, hipHostMallocDefault) == hipSuccess;
         if (!ok) {
             free_bufs(c);
+            (void)hipEventDestroy(c->ev);
             (void)hipStreamDestroy(c->stream);
             delete c;
             return LMPC_ERR_ALLOC;
@@ -165,6 +220,7 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     }
     if (max_batch > 0 && lmpc_reserve(c, max_batch) != LMPC_OK) {
         free_bufs(c);
+        (void)hipEventDestroy(c->ev);
         (void)hipStreamDestroy(c->stream);
         delete c;
         return LMPC_ERR_ALLOC;
@@ -175,9 +231,11 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
 
 void lmpc_destroy(lmpc_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    DeviceScope ds(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ev_live) (void)hipEventSynchronize(c->ev);  // the last launch on a caller's stream
     free_bufs(c);
+    if (c->ev) (void)hipEventDestroy(c->ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -207,10 +265,11 @@ int lmpc_get_dense_path(const lmpc_ctx* c) { return c ? c->prm.dense : LMPC_ERR_
 int lmpc_reserve(lmpc_ctx* c, int batch) {
     if (!c || batch < 0) return LMPC_ERR_ARG;
     if ((size_t)batch <= c->scratch_qps) return LMPC_OK;
-    if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
+    DeviceScope ds(c->device);
+    if (!ds.ok) return LMPC_ERR_DEVICE;
     if (c->d_scratch) {
         (void)hipStreamSynchronize(c->stream);
-        (void)hipDeviceSynchronize();
+        (void)hipDeviceSynchronize();  // queued launches on callers' streams may still read the old buffers
         (void)hipFree(c->d_scratch);
         (void)hipFree(c->d_done);
         c->d_scratch = nullptr;
@@ -232,20 +291,25 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
                                int batch, double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_rec || !d_contact || !d_grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
+    DeviceScope ds(c->device);
+    if (!ds.ok) return LMPC_ERR_DEVICE;
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
+    if (!stream_ok(s, c->device)) return LMPC_ERR_ARG;
     if ((size_t)batch > c->scratch_qps) {
         const int rc = lmpc_reserve(c, batch);
         if (rc != LMPC_OK) return rc;
     }
-    hipError_t e = hipSuccess;
-    // condensed dense kernel first; the Riccati kernel then skips the QPs it solved
-    if (c->prm.dense == 2)
+    hipError_t e = ctx_enter(c, s);
+    // condensed dense kernel first; it flags the QPs it solved and the Riccati kernel solves the rest
+    // (more than 20 stance leg-steps, or a dense QP left without a verified optimum)
+    if (e == hipSuccess && c->prm.dense == 2)
         e = lmpc::launch_gi(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
-    else if (c->prm.dense == 1)
-        e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, s);
+    else if (e == hipSuccess && c->prm.dense == 1)
+        e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
     if (e == hipSuccess)
         e = lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch,
-                            c->prm.dense == 2 ? c->d_done : nullptr, s);
+                            c->prm.dense ? c->d_done : nullptr, s);
+    if (e == hipSuccess) e = ctx_leave(c, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
 }
@@ -269,7 +333,8 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
             if (!(n[2] > 0.0) || !std::isfinite(n[0]) || !std::isfinite(n[1]) || !std::isfinite(n[2]))
                 return LMPC_ERR_ARG;
         }
-    if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
+    DeviceScope ds(c->device);
+    if (!ds.ok) return LMPC_ERR_DEVICE;
     hipStream_t s = c->stream;
     const bool warm = act_in || act_out;
     lmpc::DevParams prm = c->prm;
@@ -279,6 +344,9 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
     const size_t nnrm = normals ? (size_t)batch * 12 * sizeof(double) : 0;
     const size_t ncon = (size_t)batch * 4 * c->H;
     const size_t nact = act_in ? ncon : 0;
+    // the pinned staging blocks and the factor scratch may still be in use by an earlier asynchronous
+    // device-path call on another stream: wait for it before the host writes the staging block
+    if (c->ev_live && c->ev_stream != s && hipEventSynchronize(c->ev) != hipSuccess) return LMPC_ERR_DEVICE;
     std::memcpy(c->h_in, rec, nrec);
     if (normals) std::memcpy(c->h_in + nrec, normals, nnrm);
     std::memcpy(c->h_in + nrec + nnrm, contact, ncon);
@@ -289,7 +357,7 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
     const size_t nst = (size_t)batch * sizeof(int32_t);
     double* d_grf = (double*)c->d_out;
     int32_t* d_st = (int32_t*)(c->d_out + ngrf);
-    uint8_t* d_done = c->d_out + ngrf + 2 * nst;  // dual active-set flags travel back with the results
+    uint8_t* d_done = c->d_out + ngrf + 2 * nst;  // dense-path hand-over flags travel back with the results
     uint8_t* d_aout = d_done + batch;
     const double* d_rec = (const double*)c->d_in;
     const uint8_t* d_con = c->d_in + nrec + nnrm;
@@ -311,24 +379,27 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
     hipError_t e = hipSuccess;
     if (n_dense)
         e = gi ? lmpc::launch_gi(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s)
-               : lmpc::launch_dense(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, s);
+               : lmpc::launch_dense(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s);
     if (e == hipSuccess && n_ric)
         e = lmpc::launch_qp(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch,
-                            gi ? d_done : nullptr, s);
+                            prm.dense ? d_done : nullptr, s);
+    if (e == hipSuccess) e = ctx_leave(c, s);
     if (e != hipSuccess) return launch_rc(e);
-    // one copy back: [grf | status | iters], plus the done flags (dual active set) or the active set (warm)
-    const size_t nout = act_out ? ngrf + 2 * nst + batch + ncon : ngrf + 2 * nst + (gi ? (size_t)batch : 0);
+    // one copy back: [grf | status | iters], plus the hand-over flags (dense path) or the active set (warm)
+    const size_t nout = act_out ? ngrf + 2 * nst + batch + ncon : ngrf + 2 * nst + (n_dense ? (size_t)batch : 0);
     if (hipMemcpyAsync(c->h_out, c->d_out, nout, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return LMPC_ERR_DEVICE;
-    if (gi && n_dense && !n_ric) {
-        // a QP the dual active set left (step cap, non-finite step) goes to the Riccati kernel, as on the device
+    if (n_dense && !n_ric) {
+        // a QP the dense kernel left (iteration or step cap, non-finite iterate) goes to the Riccati kernel,
+        // as on the device path
         const uint8_t* hd = c->h_out + ngrf + 2 * nst;
         bool left = false;
         for (int b = 0; b < batch && !left; ++b) left = hd[b] == 0;
         if (left) {
             if ((size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
             e = lmpc::launch_qp(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch, d_done, s);
+            if (e == hipSuccess) e = ctx_leave(c, s);
             if (e != hipSuccess) return launch_rc(e);
             if (hipMemcpyAsync(c->h_out, c->d_out, ngrf + 2 * nst, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
@@ -372,11 +443,19 @@ static int launch_rc(hipError_t e) {
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
 }
 
+// Entry points that launch on the caller's stream without touching the context's buffers: device scope and
+// stream check only.
+#define LMPC_DEVICE_ENTRY(c, s)                         \
+    DeviceScope ds_(c->device);                         \
+    if (!ds_.ok) return LMPC_ERR_DEVICE;                \
+    hipStream_t s = (hipStream_t)stream; /* NULL = the HIP null stream (ordered with blocking streams) */ \
+    if (!stream_ok(s, c->device)) return LMPC_ERR_ARG
+
 int lmpc_build_records_device(lmpc_ctx* c, const lmpc_command* d_cmd, int batch, double* d_rec, uint8_t* d_contact,
                               void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_cmd || !d_rec || !d_contact))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
+    LMPC_DEVICE_ENTRY(c, s);
     return launch_rc(lmpc::launch_records(d_cmd, batch, c->H, c->prm.dt, d_rec, d_contact, s));
 }
 
@@ -384,9 +463,8 @@ int lmpc_solve_commands_device(lmpc_ctx* c, const lmpc_command* d_cmd, const dou
                                double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_cmd || !d_grf))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
+    LMPC_DEVICE_ENTRY(c, s);
     if ((size_t)batch > c->cmd_qps) {
-        if (hipSetDevice(c->device) != hipSuccess) return LMPC_ERR_DEVICE;
         (void)hipDeviceSynchronize();  // the old buffers may still be read by queued work
         (void)hipFree(c->d_crec);
         (void)hipFree(c->d_ccon);
@@ -398,8 +476,10 @@ int lmpc_solve_commands_device(lmpc_ctx* c, const lmpc_command* d_cmd, const dou
             return LMPC_ERR_ALLOC;
         c->cmd_qps = (size_t)batch;
     }
-    int rc = lmpc_build_records_device(c, d_cmd, batch, c->d_crec, c->d_ccon, s);
-    if (rc != LMPC_OK) return rc;
+    // the expansion overwrites the context's record buffers: order it behind the previous solve that read them
+    hipError_t e = ctx_enter(c, s);
+    if (e == hipSuccess) e = lmpc::launch_records(d_cmd, batch, c->H, c->prm.dt, c->d_crec, c->d_ccon, s);
+    if (e != hipSuccess) return launch_rc(e);
     return lmpc_solve_batch_device_ex(c, c->d_crec, c->d_ccon, d_normals, batch, d_grf, d_status, d_iters, s);
 }
 
@@ -407,7 +487,7 @@ int lmpc_synth_commands_device(lmpc_ctx* c, const lmpc_synth_cfg* cfg, uint64_t 
                                lmpc_command* d_cmd, void* stream) {
     if (!c || !cfg || count < 0 || (count > 0 && !d_cmd)) return LMPC_ERR_ARG;
     if (count == 0) return LMPC_OK;
-    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
+    LMPC_DEVICE_ENTRY(c, s);
     return launch_rc(lmpc::launch_synth(*cfg, seed, first_index, count, d_cmd, s));
 }
 
@@ -416,7 +496,7 @@ int lmpc_synth_normals_device(lmpc_ctx* c, uint64_t seed, int64_t first_index, i
     if (!c || count < 0 || (count > 0 && !d_normals) || !(theta_max >= 0.0) || theta_max >= 1.5707963267948966)
         return LMPC_ERR_ARG;
     if (count == 0) return LMPC_OK;
-    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
+    LMPC_DEVICE_ENTRY(c, s);
     return launch_rc(lmpc::launch_normals(seed, first_index, count, theta_max, d_normals, s));
 }
 
@@ -424,13 +504,18 @@ int lmpc_grf_to_torque_device(lmpc_ctx* c, const lmpc_leg_kin* k, const double* 
                               const double* d_grf, int batch, double* d_tau, void* stream) {
     if (!c || !k || batch < 0 || (batch > 0 && (!d_rec || !d_joint_pos || !d_grf || !d_tau))) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
+    LMPC_DEVICE_ENTRY(c, s);
     return launch_rc(lmpc::launch_torque(*k, d_rec, d_joint_pos, d_grf, batch, c->H, d_tau, s));
 }
+#undef LMPC_DEVICE_ENTRY
 
 int lmpc_sync(lmpc_ctx* c) {
     if (!c) return LMPC_ERR_ARG;
-    return hipStreamSynchronize(c->stream) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
+    DeviceScope ds(c->device);
+    if (!ds.ok) return LMPC_ERR_DEVICE;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return LMPC_ERR_DEVICE;
+    // and the last launch that used the context's buffers, whatever stream it ran on
+    return !c->ev_live || hipEventSynchronize(c->ev) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
 }
 
 }  // extern "C"

@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                                                         const uint8_t* __restrict__ contact,
                                                         const double* __restrict__ normals, int batch,
                                                         double* __restrict__ grf, int32_t* __restrict__ status,
-                                                        int32_t* __restrict__ iters) {
+                                                        int32_t* __restrict__ iters, uint8_t* __restrict__ done_out) {
     extern __shared__ __attribute__((aligned(16))) double dn_smem[];
     const int qp = blockIdx.x;
     if (qp >= batch) return;
@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
     const int lc = lane & 15, lr = lane >> 4;
     for (;;) {
         if (mode == PRED) {
+            if (ipm_it >= prm.dense_iter_cap) break;  // test hook: hand the QP to the Riccati kernel
             double loc = 0.0;
             if (st) {
 #pragma unroll
@@ -509,9 +510,19 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
         for (int m = 0; m < 3; ++m) u[m] = f[m];
     }
-    // ---- output: stance forces through LDS to the lane of leg-step 4k + j ----
     const int bad = st && (u[0] != u[0] || u[1] != u[1] || u[2] != u[2]);
     const bool anybad = __any(bad);
+    // A QP without a verified optimum (iteration caps, non-finite iterate) is left to the Riccati kernel of the
+    // same launch, as lmpc_gi_kernel does: flag 0, nothing written.  Flag 1: solved here.
+    if (done_out) {
+        const bool keep = done && !anybad;
+        if (lane == 0) done_out[qp] = keep ? 1 : 0;
+        if (!keep) {
+            DSTAMP_FLUSH(qp);
+            return;
+        }
+    }
+    // ---- output: stance forces through LDS to the lane of leg-step 4k + j ----
     LMPC_SYNC();
     if (st) {
         double fo[3] = {u[0], u[1], u[2]};
@@ -538,9 +549,9 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 }
 
 template __global__ void lmpc_dense_kernel<false>(const DevParams, const double*, const uint8_t*, const double*, int,
-                                                  double*, int32_t*, int32_t*);
+                                                  double*, int32_t*, int32_t*, uint8_t*);
 template __global__ void lmpc_dense_kernel<true>(const DevParams, const double*, const uint8_t*, const double*, int,
-                                                 double*, int32_t*, int32_t*);
+                                                 double*, int32_t*, int32_t*, uint8_t*);
 
 #ifdef LMPC_STAMPS
 extern "C" int lmpc_debug_dense_stamps(unsigned long long* out, int nqp) {
@@ -557,19 +568,19 @@ size_t dense_lds_bytes(int H) {
 }
 
 hipError_t launch_dense(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
-                        int batch, double* grf, int32_t* status, int32_t* iters, hipStream_t stream) {
+                        int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream) {
     const size_t lds = dense_lds_bytes(prm.H);
     const dim3 grid(batch), block(LMPC_WAVE);
     if (normals) {
         (void)hipFuncSetAttribute((const void*)lmpc_dense_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         hipLaunchKernelGGL(lmpc_dense_kernel<true>, grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
-                           status, iters);
+                           status, iters, done);
     } else {
         (void)hipFuncSetAttribute((const void*)lmpc_dense_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         hipLaunchKernelGGL(lmpc_dense_kernel<false>, grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
-                           status, iters);
+                           status, iters, done);
     }
     return hipGetLastError();
 }

@@ -25,6 +25,8 @@ struct DevParams {
     int dense;         // QPs with 1..DENSE_MAX_LS stance leg-steps: 0 Riccati kernel, 1 condensed interior
                        // point (lmpc_dense.hip), 2 condensed dual active set (lmpc_gi.hip)
     int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel
+    int dense_iter_cap;  // condensed interior point: IPM iterations after which a QP is handed to the Riccati
+                         // kernel (test hook LMPC_DENSE_ITER_CAP; default: never, max_iter governs)
     int cus;           // compute units of the device (launch shaping only)
     // warm start of the Riccati kernel (per QP and leg-step [B][H][4]: bits 0-4 = active pyramid faces and
     // bound, 15 = lift-off apex).  warm_act != nullptr: the kernel starts in the active-set polish from it and

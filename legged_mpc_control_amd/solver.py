@@ -362,11 +362,25 @@ class ConvexQPSolver:
         p.mu, p.f_max, p.gravity, p.dt = float(mu), float(f_max), float(gravity), float(dt)
         self.H = int(horizon)
         self._p = p
-        # one QP per call: the dual active-set kernel has the lower latency (no batch tail)
+        # Same defaults as the C++ drop-in (legged::ConvexQPSolver): warm start on, so every tick runs on the
+        # Riccati kernel from the previous tick's verified active set shifted one step (the reference's OSQP
+        # warm-starts too, ConvexQPSolver.cpp:185); cold solves (set_warm_start(False)) take the dual active
+        # set, the lower-latency dense kernel for one QP per call.
         self._dev = BatchedConvexQPSolver(p, self.H, 1, device, dense_path="gi")
         self._rec = np.zeros((1, 33 + 12 * self.H))
         self._con = np.ones((1, self.H, 4), dtype=np.uint8)
+        self._warm = True
+        self._act = None  # last verified active set [1, H, 4]
         self.last_status = 0
+        self.last_iterations = 0
+
+    def set_warm_start(self, on: bool) -> None:
+        self._warm = bool(on)
+        self._act = None
+
+    @property
+    def warm_start(self) -> bool:
+        return self._warm
 
     def calc_mpc_reference(self, state: LeggedState, leg_FSM) -> None:
         st = N.LmpcStateIn()
@@ -395,7 +409,13 @@ class ConvexQPSolver:
         """No-op: the constraint values are built on the device inside the solve."""
 
     def compute_grfs(self, state: LeggedState) -> np.ndarray:
-        grf, status, _ = self._dev.solve(self._rec, self._con)
+        if self._warm:
+            act_in = None if self._act is None else BatchedConvexQPSolver.shift_active_set(self._act)
+            grf, status, iters, act = self._dev.solve_warm(self._rec, self._con, act_in)
+            self._act = act if int(status[0]) == 0 else None
+        else:
+            grf, status, iters = self._dev.solve(self._rec, self._con)
         self.last_status = int(status[0])
+        self.last_iterations = int(iters[0])
         self.last_solution = grf[0]
         return grf[0, 0].copy()  # u_0: FL, FR, RL, RR x (fx, fy, fz), world frame

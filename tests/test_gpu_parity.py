@@ -500,3 +500,114 @@ def test_warm_start(cid):
     assert np.all(stj == 0) and rel_err(gj, ref) <= TOL_REGRESS
     sh = BatchedConvexQPSolver.shift_active_set(a0)
     assert np.array_equal(sh[:, :-1], a0[:, 1:]) and np.array_equal(sh[:, -1], a0[:, -1])
+
+
+@pytest.mark.parametrize("path", ["host", "device"])
+def test_ipm_iteration_cap_hands_over_to_riccati(path, torch_dev, monkeypatch):
+    """A condensed interior-point QP left without a verified optimum is solved by the Riccati kernel in the same
+    call, as the dual active set's are: with the dense kernel capped at 3 iterations (test hook
+    LMPC_DENSE_ITER_CAP) every config-2 QP is handed over, so the answer, status and iteration word are the
+    Riccati kernel's own, bit for bit."""
+    import torch
+
+    p, H, rec, con = synth.config_batch(2, count=256, first_index=606)
+
+    def run():
+        s = BatchedConvexQPSolver(p, H, max_batch=256)
+        if path == "host":
+            return s.solve(rec, con)
+        out = torch.empty((256, H, 12), dtype=torch.float64, device=torch_dev)
+        st = torch.empty(256, dtype=torch.int32, device=torch_dev)
+        it = torch.empty(256, dtype=torch.int32, device=torch_dev)
+        s.solve_device(torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev), out, st, it)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
+
+    monkeypatch.setenv("LMPC_DENSE", "ipm")
+    monkeypatch.setenv("LMPC_DENSE_ITER_CAP", "3")
+    gc, sc, ic = run()
+    monkeypatch.delenv("LMPC_DENSE_ITER_CAP")
+    gd, sd, idn = run()
+    monkeypatch.setenv("LMPC_DENSE", "0")
+    gr, sr, ir = run()
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
+    assert fails == 0 and np.all(sc == 0) and np.all(sd == 0) and np.all(sr == 0)
+    assert np.all((idn & 0xFFFF) > 3)                       # uncapped: every QP needs more than 3 iterations
+    assert np.array_equal(gc, gr) and np.array_equal(ic, ir)  # capped: all solved by the Riccati kernel
+    assert rel_err(gc, ref) <= TOL_REGRESS and rel_err(gd, ref) <= TOL_REGRESS
+
+
+def test_mixed_streams_and_host_path_share_one_context(torch_dev, monkeypatch):
+    """One context, three calls in flight: an asynchronous device solve on stream A (Riccati kernel: per-QP
+    factor scratch), a host-pointer solve (the context's own stream, same scratch slots) issued before A has
+    finished, then a device solve on stream B.  The context orders them, so each result equals the
+    same solve run alone.  The caller's current device is left as it was."""
+    import torch
+
+    monkeypatch.setenv("LMPC_DENSE", "0")
+    p, H, rec, con = synth.config_batch(3, count=4096, first_index=1)    # H = 20: ~7 ms of Riccati kernel
+    _, _, rec2, con2 = synth.config_batch(3, count=512, first_index=90001)
+    _, _, rec3, con3 = synth.config_batch(3, count=2048, first_index=50001)
+    s = BatchedConvexQPSolver(p, H, max_batch=512)
+
+    def alone_device(r, c):
+        out = torch.empty((r.shape[0], H, 12), dtype=torch.float64, device=torch_dev)
+        s.solve_device(torch.from_numpy(r).to(torch_dev), torch.from_numpy(c).to(torch_dev), out)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    ref1, ref3 = alone_device(rec, con), alone_device(rec3, con3)
+    ref2, st2, _ = s.solve(rec2, con2)
+    assert np.all(st2 == 0)
+    dev_before = torch.cuda.current_device()
+    a, b = torch.cuda.Stream(torch_dev), torch.cuda.Stream(torch_dev)
+    d1 = (torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev))
+    d3 = (torch.from_numpy(rec3).to(torch_dev), torch.from_numpy(con3).to(torch_dev))
+    torch.cuda.synchronize()
+    o1 = torch.empty((rec.shape[0], H, 12), dtype=torch.float64, device=torch_dev)
+    o3 = torch.empty((rec3.shape[0], H, 12), dtype=torch.float64, device=torch_dev)
+    s.solve_device(d1[0], d1[1], o1, stream=a)      # returns at once; the kernel runs for milliseconds
+    g2, st2b, _ = s.solve(rec2, con2)              # host path on the context's stream, same scratch slots
+    s.solve_device(d3[0], d3[1], o3, stream=b)
+    torch.cuda.synchronize()
+    assert torch.cuda.current_device() == dev_before
+    assert np.array_equal(o1.cpu().numpy(), ref1)
+    assert np.array_equal(g2, ref2) and np.all(st2b == 0)
+    assert np.array_equal(o3.cpu().numpy(), ref3)
+
+
+def test_python_dropin_warm_ticks_match_oracle():
+    """The Python drop-in warm-starts by default, like the C++ one: over consecutive ticks of a trot (FSM phase
+    advancing, state drifting) every tick's u_0 equals the oracle's, and the later ticks re-verify the shifted
+    active set with few interior-point iterations."""
+    from legged_mpc_control_amd import ConvexQPSolver, LeggedContactFSM, LeggedState
+
+    p = synth.params("go1")
+    H = 10
+    solver = ConvexQPSolver(p.q_weights, p.r_weights, horizon=H)
+    assert solver.warm_start
+    st = LeggedState()
+    st.param.gait_counter_speed = 4.0
+    fsm = [LeggedContactFSM() for _ in range(4)]
+    for i in range(4):
+        fsm[i].reset_params(st, i)
+        fsm[i].gait_phase = 0.1
+    feet = np.array([[0.17, 0.12, -0.3], [0.17, -0.17, -0.3], [-0.17, 0.17, -0.3], [-0.17, -0.12, -0.3]]).T
+    st.ctrl.root_pos_d = np.array([0, 0, 0.28])
+    st.ctrl.root_lin_vel_d_rel = np.array([0.4, 0.0, 0.0])
+    op = O.params_from(p)
+    ipm = []
+    for tick in range(6):
+        st.fbk.root_pos = np.array([0.004 * tick, 0.0, 0.27])
+        st.fbk.root_lin_vel = np.array([0.4, 0.0, 0.0])
+        st.fbk.foot_pos_abs = feet
+        for i in range(4):
+            st.ctrl.plan_contacts[i] = bool(fsm[i].get_contact_state())
+        solver.calc_mpc_reference(st, fsm)
+        u0 = solver.compute_grfs(st)
+        ref, _, _ = O.solve(op, H, solver._rec[0], solver._con[0])
+        assert solver.last_status == 0 and rel_err(u0, ref[0]) <= TOL_REGRESS, tick
+        ipm.append(solver.last_iterations & 0xFFFF)
+        for i in range(4):
+            fsm[i].gait_phase = (fsm[i].gait_phase + 4.0 * 0.01) % 1.0
+    assert ipm[0] > 0 and min(ipm[1:]) == 0  # tick 0 cold; later ticks start from the shifted verified set
