@@ -11,6 +11,10 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "liblmpc.so")
 ARCH = "gfx950"
+# MFMA accumulators in the VGPR file (gfx950's register file is unified): without it the compiler parks the
+# fp64 MFMA results in AGPRs and moves every element the VALU touches with v_accvgpr_read/write.  Measured:
+# config 2 0.342 -> 0.329 ms, config 4 22.4 -> 22.0 ms (profiles/r02/diag_ab_configs.log).
+HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
 HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h"]
@@ -33,13 +37,14 @@ def _stale(target: str, deps) -> bool:
 def build_native(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [
-        os.path.join(ROOT, "include", "lmpc", "lmpc.h"), os.path.join(ROOT, "include", "lmpc", "ConvexQPSolver.hpp")]
+        os.path.join(ROOT, "include", "lmpc", "lmpc.h"), os.path.join(ROOT, "include", "lmpc", "ConvexQPSolver.hpp"),
+        os.path.abspath(__file__)]
     if not force and not _stale(LIB, deps):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp] + srcs
+           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp] + HIP_FLAGS + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -55,7 +60,7 @@ def build_stamps(force: bool = False) -> str:
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-DLMPC_STAMPS",
-           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + srcs
+           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + HIP_FLAGS + srcs
     subprocess.run(cmd, check=True)
     return out
 
@@ -68,7 +73,7 @@ def build_variant(tag: str, defines, force: bool = False) -> str:
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + [f"-D{d}" for d in defines] + srcs
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + HIP_FLAGS + [f"-D{d}" for d in defines] + srcs
     subprocess.run(cmd, check=True)
     return out
 

@@ -17,8 +17,9 @@
 //
 // Newton system (H + C'WC) u = -(g + C'W(s-b)) (IPM) or T'HT y = -T'(H up + g) (polish), solved by
 // a tiled Cholesky M = U'U on the fp64 matrix cores:
-//   diagonal tile   16x16 block Cholesky by leg blocks (3x3 pivots, VALU, one column per lane,
-//                   [M_bb | I] -> U_bb^-1) -- the only serial part;
+//   diagonal tile   16x16 block Cholesky by leg blocks (3x3 pivots) with U_bb^-T = L^-1 built alongside:
+//                   per pivot one rank-3 MFMA update of the tile and one of L^-1 (diag_inverse) -- the
+//                   only serial part;
 //   row panel       U_bc = U_bb^-T M_bc and its transpose (v_mfma_f64_16x16x4f64, X'Y form);
 //   trailing        M_cd -= U_bc' U_bd;
 //   solves          U'y = r, U x = y tile by tile on the matrix cores (vectors replicated across

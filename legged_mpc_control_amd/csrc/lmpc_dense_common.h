@@ -82,12 +82,12 @@ struct DSmem {
     ldouble* act;   // 20: 1 = leg-step coupled (T != 0)
     ldouble* lup;   // 60: polish particular solution up per leg-step (kept out of registers)
     ldouble* lua;   // 60: predictor step u_aff per leg-step
-    ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | el(272) PNL(96) L^-1(272)
+    ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | diag_inverse: pivot rows (96) W' (272) sink (112)
     lint* lsm;      // 20: stance leg-step b -> 4k + j
     lint* fb;       // H+1: first stance leg-step of step k
 };
-constexpr int DN_EL = 16 * 17;                // staging of one 16x16 tile, column stride 17
-constexpr int DN_SCR_MIN = DN_EL + 96 + DN_EL;  // el | PNL | L^-1
+constexpr int DN_EL = 16 * 17;               // staging of one 16x16 tile, column stride 17
+constexpr int DN_SCR_MIN = 96 + DN_EL + 112;  // diag_inverse: pivot rows | W' | store sink
 
 __device__ __forceinline__ DSmem dcarve(double* sm, int H) {
     DSmem s;
@@ -283,8 +283,19 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
 
 // ---------------------------------------------------------------------------
 // Diagonal tile: U_bb^-1 (Ui, = L^-T) and its transpose (UiT, = L^-1) of M_bb = L L'.
-// Block Cholesky by leg blocks (3x3 pivots) on [M_bb | I], one column per lane (lanes 0-31),
-// decoupled identity blocks (unused / padding / apex legs) skipped.  amask: coupled blocks (bits 0-4).
+// Block Cholesky by leg blocks (3x3 pivots), decoupled identity blocks (unused / padding / apex legs)
+// skipped.  amask: coupled blocks (bits 0-4).
+//
+// The tile T and W = L^-1 (from I) stay in the MFMA accumulator layout (lane 16g + c, register i <->
+// element (4i + g, c)).  Per pivot block P = T[o..o+2][o..o+2] (o = 3 blk):
+//   the three pivot rows of T and W go through LDS once (one write -> read round trip);
+//   every lane factors P = L_p L_p' itself (3 rsq + Newton);
+//   lane 16k + m forms L_C[m][k] = (L_p^-1 T[o..o+2][m])_k for the rows m below the pivot (T symmetric)
+//   and (L_p^-1 W[o..o+2][c])_k -- the MFMA A and B operands;
+//   trailing update T -= L_C L_C' and W -= L_C (L_p^-1 W_p): one v_mfma_f64_16x16x4f64 each (rank 3 of 4);
+//   the pivot rows of W become L_p^-1 W_p (Gauss-Jordan on [L | I]: W = L_n^-1 ... L_1^-1 = L^-1).
+// Per pivot: 2 MFMAs, one LDS round trip, ~40 VALU -- the row-by-row elimination it replaces (one column
+// per lane, three broadcast LDS reads per row and pivot) issued ~5x the LDS reads.
 // ---------------------------------------------------------------------------
 struct DiagInv {
     d4 ui, uit;
@@ -292,86 +303,86 @@ struct DiagInv {
 // Outlined (one call site): the elimination gets the caller-saved registers to itself instead of
 // competing with the factor tiles and the leg state that are live around it.
 static __device__ __attribute__((noinline)) DiagInv diag_inverse(ldouble* scr, d4 M, int amask, int lane) {
-    // column-major staging with an odd column stride (17 doubles): a wave's 16 columns fall on
-    // distinct LDS banks (a stride of 16 puts them on two banks: 8-way conflicts)
-    ldouble* el = scr;
-    ldouble* PNL = scr + DN_EL;
-    ldouble* li = scr + DN_EL + 96;
-    const int lc = lane & 15, lr = lane >> 4;
+    ldouble* pv = scr;              // 96: pivot rows o..o+2 of T (48) then of W (48), 16 columns each
+    ldouble* tr = scr + 96;         // 16 x 17: transpose staging of W
+    ldouble* dummy = scr + 96 + 272;  // 112: sink of the stores of lanes that hold no pivot row
+    const int c = lane & 15, g = lane >> 4;
+    d4 T = M, W;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) el[lc * 17 + lr + 4 * i] = M[i];
-    LMPC_SYNC();
-    double a[16];
-    {
-        const ldouble* src = el + 17 * (lane < 16 ? lane : 0);
-        const double keep = (lane < 16) ? 1.0 : 0.0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a[r] = fma(src[r], keep, (r == lane - 16) ? 1.0 : 0.0);
-    }
-    if (amask) {
-        const int b0 = __builtin_ctz(amask);
-        if (lane >= 3 * b0 && lane < 3 * b0 + 3) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) PNL[(lane - 3 * b0) * 16 + r] = a[r];
-        }
-    }
-    int par = 0;
+    for (int i = 0; i < 4; ++i) W[i] = (4 * i + g == c) ? 1.0 : 0.0;
 #pragma unroll
     for (int blk = 0; blk < 5; ++blk) {
         if (!((amask >> blk) & 1)) continue;
         const int o = 3 * blk;
-        const ldouble* pnl = PNL + par * 48;
+        // rows o..o+2 live in registers i0 = o>>2 and i1 = (o+2)>>2 (static); this lane's row of register i is 4i+g
+        const int i0 = o >> 2, i1 = (o + 2) >> 2;
+        const int ra = 4 * i0 + g - o, rb = 4 * i1 + g - o;
+        const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
         LMPC_SYNC();
-        const double i00 = rsq_nr(pnl[o]);
-        const double l10 = pnl[o + 1] * i00, l20 = pnl[o + 2] * i00;
-        const double i11 = rsq_nr(pnl[16 + o + 1] - l10 * l10);
-        const double l21 = (pnl[16 + o + 2] - l20 * l10) * i11;
-        const double i22 = rsq_nr(pnl[32 + o + 2] - l20 * l20 - l21 * l21);
-        const double z0 = i00 * a[o];
-        const double z1 = (a[o + 1] - l10 * z0) * i11;
-        const double z2 = (a[o + 2] - l20 * z0 - l21 * z1) * i22;
-        const int rest = amask >> (blk + 1);
-        if (blk < 4 && rest) {
-            const double y2 = z2 * i22;
-            const double y1 = (z1 - l21 * y2) * i11;
-            const double y0 = (z0 - l10 * y1 - l20 * y2) * i00;
-            const int nb = blk + 1 + __builtin_ctz(rest);
-#pragma unroll
-            for (int r = o + 3; r < o + 6; ++r) a[r] -= pnl[r] * y0 + pnl[16 + r] * y1 + pnl[32 + r] * y2;
-            const bool pub = lane >= 3 * nb && lane < 3 * nb + 3;
-            ldouble* nx = PNL + (par ^ 1) * 48 + (pub ? (lane - 3 * nb) * 16 : 0);
-            if (pub && nb == blk + 1) {
-#pragma unroll
-                for (int r = o + 3; r < o + 6; ++r) nx[r] = a[r];
-            }
-#pragma unroll
-            for (int r = o + 6; r < 15; ++r) a[r] -= pnl[r] * y0 + pnl[16 + r] * y1 + pnl[32 + r] * y2;
-            if (pub) {
-#pragma unroll
-                for (int r = o + 6; r < 15; ++r) nx[r] = a[r];
+        // publish the pivot rows of T first (unconditional stores; lanes without a pivot row store to the sink):
+        // the T chain of this pivot waits only for the previous T update, not for the W update issued after it
+        {
+            ldouble* da = ina ? pv + 16 * ra + c : dummy + lane;
+            da[0] = T[i0];
+            if (i1 != i0) {
+                ldouble* db = inb ? pv + 16 * rb + c : dummy + lane;
+                db[0] = T[i1];
             }
         }
-        a[o] = z0;
-        a[o + 1] = z1;
-        a[o + 2] = z2;
-        par ^= 1;
+        LMPC_SYNC();
+        const double p00 = pv[o], p10 = pv[16 + o], p11 = pv[16 + o + 1];
+        const double p20 = pv[32 + o], p21 = pv[32 + o + 1], p22 = pv[32 + o + 2];
+        const double t0 = pv[c], t1 = pv[16 + c], t2 = pv[32 + c];               // T[o+a][c] = T[c][o+a]
+        // then the pivot rows of W (+48), read while the pivot is factored; W's pivot rows are cleared so the
+        // MFMA below writes L_p^-1 W_p into them
+        {
+            ldouble* da = ina ? pv + 48 + 16 * ra + c : dummy + 48 + lane;
+            da[0] = W[i0];
+            W[i0] = ina ? 0.0 : W[i0];
+            if (i1 != i0) {
+                ldouble* db = inb ? pv + 48 + 16 * rb + c : dummy + 48 + lane;
+                db[0] = W[i1];
+                W[i1] = inb ? 0.0 : W[i1];
+            }
+        }
+        LMPC_SYNC();
+        const double w0 = pv[48 + c], w1 = pv[64 + c], w2 = pv[80 + c];          // W[o+a][c]
+        const double i00 = rsq_nr(p00);
+        const double l10 = p10 * i00, l20 = p20 * i00;
+        const double i11 = rsq_nr(fma(-l10, l10, p11));
+        const double l21 = fma(-l20, l10, p21) * i11;
+        const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
+        // row c of L_C (zero in and above the pivot rows)
+        const double x0 = t0 * i00;
+        const double x1 = fma(-l10, x0, t1) * i11;
+        const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
+        const double xs = g == 0 ? x0 : g == 1 ? x1 : x2;
+        const double av = (c > o + 2 && g < 3) ? xs : 0.0;
+        // column c of L_p^-1 W_p
+        const double v0 = w0 * i00;
+        const double v1 = fma(-l10, v0, w1) * i11;
+        const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
+        const double vs = g == 0 ? v0 : g == 1 ? v1 : v2;
+        const double bv = g < 3 ? vs : 0.0;
+        // W's A operand: -L_C below the pivot, the unit rows of the pivot block (W_new pivot rows = L_p^-1 W_p)
+        const bool cp = c >= o && c <= o + 2;
+        const double aw = cp ? (g == c - o ? 1.0 : 0.0) : -av;
+        T = MFMA64(-av, av, T);
+        W = MFMA64(aw, bv, W);
     }
-    // lanes 16+c hold column c of L^-1: stage it (stride 17), then read both tile orientations
-    if (lane >= 16 && lane < 32) {
-        const int c = lane - 16;
+    // W = L^-1 (lower triangular): uit = W; ui = W' through LDS (column stride 17: distinct banks)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) li[c * 17 + r] = a[r];
-    }
+    for (int i = 0; i < 4; ++i) tr[c * 17 + 4 * i + g] = W[i];
     LMPC_SYNC();
     DiagInv out;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r = lr + 4 * i;
-        out.uit[i] = li[lc * 17 + r];  // (r, c) = L^-1[r][c]
-        out.ui[i] = li[r * 17 + lc];   // (r, c) = L^-1[c][r]
+        out.uit[i] = W[i];
+        out.ui[i] = tr[(4 * i + g) * 17 + c];
     }
     return out;
 }
+
 
 // coupled-block mask of tile t (bits 0-4: leg-steps 5t..5t+4 valid, and with use_act also coupled)
 __device__ __forceinline__ int tile_mask(const DSmem& S, int t, int nls, bool use_act) {

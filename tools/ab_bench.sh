@@ -1,0 +1,13 @@
+#!/bin/bash
+# Dev tool (GPU box): A/B kernel times of diagnostic library builds over the bench configs.
+#   tools/ab_bench.sh TAG [TAG ...]   (libraries tools/build/liblmpc_TAG.so, built beforehand)
+for tag in "$@"; do
+  for spec in "2 20" "2gi 20" "3 5" "4 3" "5 5"; do
+    set -- $spec
+    cfg=${1%gi}; steps=$2
+    env=""
+    [ "$1" != "$cfg" ] && env="LMPC_DENSE=gi"
+    out=$(env $env LMPC_LIB=tools/build/liblmpc_$tag.so timeout -k 10 120 python bench.py --config $cfg --steps $steps --warmup 2 --no-cpu 2>/dev/null) || { echo "$tag config $1 FAILED"; exit 1; }
+    echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', 'config', '$1', 'kernel_ms %.4f'%d['roofline']['kernel_ms'], 'QP/s %.3e'%d['value'], 'err %.1e'%d['max_grf_err'], d['qp_status'])"
+  done
+done
