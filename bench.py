@@ -97,7 +97,12 @@ def main():
     # Inputs are generated ON THE DEVICE from (seed, global index): every rank builds its own shard in
     # HBM, no input bytes cross PCIe or xGMI.  Commands -> records + contact schedules
     # by the expansion kernel (8f-1); the timed step below is the QP solve over those records.
-    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank)
+    # Dense-path kernel per workload (fixed per context, so no answer depends on it): the interior point when every
+    # SIMD holds about one QP and the launch waits for the slowest (configs 2/3/5), the dual active set -- half the
+    # mean cost, a longer tail -- when each SIMD streams through many QPs (config 4: 64 per SIMD); DESIGN.md 4b.
+    # LMPC_DENSE, when set, overrides it.
+    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank,
+                                   dense_path="gi" if args.config == 4 else "ipm")
     seed = synth.BASE_SEED + args.config
     d_cmd = solver.synth_commands_device(synth.config_cfg(args.config), B, seed, first_index=first, device=dev)
     d_nrm = solver.synth_normals_device(B, seed, first_index=first, device=dev) if terrain else None

@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
         lk = id >> 2;
         lj = id & 3;
     }
-    double f[3], s[5], z[5];
+    double f[3], s[5], z[5], is[5];  // is = 1/s, refreshed whenever s changes (used 4x per iteration)
     {
         const double cnt = st ? (double)(S.fb[lk + 1] - S.fb[lk]) : 1.0;
         f[0] = f[1] = 0.0;
@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
         for (int i = 0; i < 5; ++i) {
             s[i] = st ? -o[i] : 1.0;
             z[i] = 1.0 / s[i];
+            is[i] = z[i];
         }
     }
     double u[3] = {0.0, 0.0, 0.0}, rt[3] = {0.0, 0.0, 0.0};
@@ -144,7 +145,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 if (st) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) {
-                        W[i] = z[i] * rcp_nr(s[i]);
+                        W[i] = z[i] * is[i];
                         wv[i] = W[i] * (s[i] - (i == 4 ? fzmax : 0.0));
                     }
                 }
@@ -388,7 +389,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                 for (int i = 0; i < 5; ++i) {
                     dsa[i] = -o[i] - s[i];
-                    dza[i] = -z[i] - z[i] * rcp_nr(s[i]) * dsa[i];
+                    dza[i] = -z[i] - z[i] * is[i] * dsa[i];
                     if (dsa[i] < 0.0) amax = fmin(amax, -s[i] * __builtin_amdgcn_rcp(dsa[i]));
                     if (dza[i] < 0.0) amax = fmin(amax, -z[i] * __builtin_amdgcn_rcp(dza[i]));
                 }
@@ -405,7 +406,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 double wv[5];
 #pragma unroll
                 for (int i = 0; i < 5; ++i)
-                    wv[i] = (z[i] * (s[i] - (i == 4 ? fzmax : 0.0)) + smu - dsa[i] * dza[i]) * rcp_nr(s[i]);
+                    wv[i] = (z[i] * (s[i] - (i == 4 ? fzmax : 0.0)) + smu - dsa[i] * dza[i]) * is[i];
                 cons_tw(wv, mu, rt);
             }
             mode = CORR;
@@ -422,11 +423,10 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 cons_resid(ua, mu, fzmax, oa);
 #pragma unroll
                 for (int i = 0; i < 5; ++i) {
-                    const double is = rcp_nr(s[i]);
                     const double dsa = -oa[i] - s[i];
-                    const double dza = -z[i] - z[i] * is * dsa;
+                    const double dza = -z[i] - z[i] * is[i] * dsa;
                     ds[i] = -o[i] - s[i];
-                    dz[i] = (smu - z[i] * s[i] - dsa * dza - z[i] * ds[i]) * is;
+                    dz[i] = (smu - z[i] * s[i] - dsa * dza - z[i] * ds[i]) * is[i];
                     if (ds[i] < 0.0) amax = fmin(amax, -s[i] * __builtin_amdgcn_rcp(ds[i]));
                     if (dz[i] < 0.0) amax = fmin(amax, -z[i] * __builtin_amdgcn_rcp(dz[i]));
                 }
@@ -439,6 +439,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 for (int i = 0; i < 5; ++i) {
                     s[i] += alpha * ds[i];
                     z[i] += alpha * dz[i];
+                    is[i] = rcp_nr(s[i]);
                 }
             }
             ++ipm_it;
