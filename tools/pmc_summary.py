@@ -23,7 +23,7 @@ def rows(name):
     return list(csv.DictReader(open(os.path.join(SRC, name, f"{name}_counter_collection.csv"))))
 
 
-SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_qp_kernel")  # one solve launch = both (the second skips the first's QPs)
+SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_gi_kernel", "lmpc_qp_kernel")  # one solve launch = a dense-path kernel + the Riccati kernel
 
 
 def per_kernel(name, kern):
@@ -65,7 +65,7 @@ def main():
             "write_bytes": wb,
             "source": f"profiles/{TAG}/pmc_per_dispatch.json",
             "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py "
-                      f"(config {c}, --no-cpu); per-dispatch means of lmpc_dense_kernel + lmpc_qp_kernel; FETCH_SIZE x {read_factor:.3f}, "
+                      f"(config {c}, --no-cpu); per-dispatch means of the launch's dense-path kernel + lmpc_qp_kernel; FETCH_SIZE x {read_factor:.3f}, "
                       f"WRITE_SIZE x {write_factor:.3f} from profiles/{TAG}/pmc_calibration.json",
         }
     json.dump(per, open(os.path.join(DST, "pmc_per_dispatch.json"), "w"), indent=1)

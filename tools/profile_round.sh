@@ -5,6 +5,7 @@
 #   (tools/ubench/pmc_cal.hip).  Every GPU step has its own limit and the chain stops at the first failure.
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
+rm -rf $OUT
 mkdir -p $OUT
 rp() { timeout -k 10 300 rocprofv3 "$@"; }
 rp --kernel-trace --stats -d $OUT/c2 -o c2 --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu > $OUT/c2_bench.log 2>&1 &&
