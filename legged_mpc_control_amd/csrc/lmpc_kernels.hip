@@ -270,14 +270,14 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         const int r = lr + 4 * i;
         roff[i] = (r < 12 && lc < 12 && (r / 3) == (lc / 3)) ? GO_RR + (r / 3) * 9 + (r % 3) * 3 + (lc % 3) : GO_ZERO;
     }
-    // K^ operand: column lc-6 of V for lc in 6-11, else the zero block
-    const ldouble* vop = (lc >= 6 && lc < 12) ? S.VL + (lc - 6) * 12 + lr : S.zero;
-    // row m of Bt for the elimination lanes 12-17 (others: row 0, blended out)
-    const int btrow = GO_BT + 12 * ((lane >= 12 && lane < 18) ? lane - 12 : 0);
-    const double btkeep = (lane >= 12 && lane < 18) ? 1.0 : 0.0;
+    // Bt' in columns 6-11 of the V^ tile (accumulator layout): lane (lr, lc), register i <- Bt[lc-6][lr+4i]
+    const bool vcol = lc >= 6 && lc < 12;
+    int btof[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) btof[i] = vcol ? GO_BT + (lc - 6) * 12 + lr + 4 * i : GO_ZERO;
     // the global operands of a stage do not depend on P: fetched one stage ahead, their latency
     // hides behind the previous stage's products
-    double bgn[2], rgn[4], btn[12], agn[4];
+    double bgn[2], rgn[4], btn[3], agn[4];
     auto fetch = [&](const gdouble* g) {
         bgn[0] = g[boff[0]];
         bgn[1] = g[boff[1]];
@@ -286,28 +286,26 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 #pragma unroll
         for (int i = 0; i < 4; ++i) rgn[i] = g[roff[i]];
 #pragma unroll
-        for (int r = 0; r < 12; ++r) btn[r] = g[btrow + r];
+        for (int i = 0; i < 3; ++i) btn[i] = g[btof[i]];
     };
     fetch(gs + (H - 1) * GS);
-    // lane-static destinations of the elimination output (hoisted so the stores stay branch-free)
-    int oofs[12];
-    ldouble* vl;
-    int vstep;
-    {
-        const bool isv = lane >= 12 && lane < 18, isl = lane >= 18 && lane < 30;
-        const int m = isv ? lane - 12 : 0, c = isl ? lane - 18 : 0;
+    // lane-static destinations of the factor outputs (branch-free stores; the rest go to the dummy word):
+    // V column m = lc - 6 contiguous (GO_V), packed lower L^-1 row r = lr + 4i, column lc <= r (GO_LINV)
+    int vofs[3], lofs[3];
 #pragma unroll
-        for (int r = 0; r < 12; ++r)
-            oofs[r] = isv ? GO_V + m * 12 + r : (isl && r >= c) ? GO_LINV + r * (r + 1) / 2 + c : GO_DUMMY;
-        vl = isv ? S.VL + m * 12 : S.pb;
-        vstep = isv ? 1 : 0;
+    for (int i = 0; i < 3; ++i) {
+        const int r = lr + 4 * i;
+        vofs[i] = vcol ? GO_V + (lc - 6) * 12 + r : GO_DUMMY;
+        lofs[i] = (lc <= r) ? GO_LINV + r * (r + 1) / 2 + lc : GO_DUMMY;
     }
+    ldouble* const pv = S.GT;     // 144: pivot rows of Guu, L^-1 and V^ (48 each)
+    ldouble* const sink = S.PNL;  // 64: stores of lanes that hold no pivot row
     SUB_DECL
     for (int k = H - 1; k >= 0; --k) {
         const double ck = S.cs[2 * k], sk = S.cs[2 * k + 1];
         ldouble* sl = S.st + k * SK;
         gdouble* g = gs + k * GS;
-        double bg[2], rg[4], bt[12], ag[4];
+        double bg[2], rg[4], bt[3], ag[4];
 #pragma unroll
         for (int i = 0; i < 2; ++i) bg[i] = bgn[i];
 #pragma unroll
@@ -315,7 +313,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 #pragma unroll
         for (int i = 0; i < 4; ++i) rg[i] = rgn[i];
 #pragma unroll
-        for (int r = 0; r < 12; ++r) bt[r] = btn[r];
+        for (int i = 0; i < 3; ++i) bt[i] = btn[i];
         // ---- operands: dt N(yaw) (k-blocks 0-1: rows 0-7) and B^ (k-blocks 1-2) ----
         double nh[2], bh[2];
 #pragma unroll
@@ -339,106 +337,114 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
         __builtin_amdgcn_sched_barrier(0);
         fetch(gs + (k > 0 ? k - 1 : 0) * GS);
         __builtin_amdgcn_sched_barrier(0);
-        // ---- out: v = C^[:, 12], Guu column-major for the elimination, Z = rows 6-11 of PA ----
+        // ---- out: v = C^[:, 12], Z = rows 6-11 of PA ----
         if (lc < 12) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
+            for (int i = 1; i < 3; ++i) {
                 const int r = lr + 4 * i;
-                S.GT[lc * 12 + r] = G[i];
                 if (r >= 6) g[GO_Z + (r - 6) * 12 + lc] = PA[i];
             }
         } else if (lc == 12) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) sl[SO_VV + lr + 4 * i] = C[i];
         }
-        LMPC_SYNC();
         SUB(5);
-        // ---- block Cholesky elimination of [Guu | Bt' | I] -> [L' | V = L^-1 Bt' | L^-1] ----
-        // lane j < 30 keeps column j in registers.  Per 3x3 leg block (one barrier each):
-        // the pivot columns go to LDS; every lane factors the pivot block D = Ld Ld' itself,
-        // keeps z = Ld^-1 x as its final block rows and subtracts G_rb D^-1 x = G_rb Ld^-T z
-        // from the rows below, reading G_rb straight from the pivot columns.
-        double a[12];
-        {
-            const ldouble* src = S.GT + 12 * (lane < 12 ? lane : 0);
-            const double keep = (lane < 12) ? 1.0 : 0.0;  // blend, not select: keeps the loads unconditional
+        // ---- block Cholesky of Guu by legs, with L^-1 (from I) and V^ = L^-1 [0 | Bt'] eliminated alongside,
+        //      all three 16x16 tiles in the accumulator layout (the dense path's diag_inverse, lmpc_dense_common.h).
+        // Per coupled 3x3 leg block: its rows of the three tiles go through LDS, every lane factors the pivot
+        // P = L_p L_p', and one rank-3 v_mfma_f64_16x16x4f64 per tile applies it: Guu -= L_C L_C', and
+        // L^-1, V^ -= L_C (L_p^-1 X_p) with their pivot rows replaced by L_p^-1 X_p.  Leg blocks with T = 0
+        // (swing legs; apex legs in the polish) have Guu block = I and no coupling: skipped (amask, wave-uniform).
+        d4 Tg, Li, X;
 #pragma unroll
-            for (int r = 0; r < 12; ++r) a[r] = fma(src[r], keep, fma(bt[r], btkeep, (r == lane - 18) ? 1.0 : 0.0));
+        for (int i = 0; i < 4; ++i) {
+            const int r = lr + 4 * i;
+            Tg[i] = (r < 12 && lc < 12) ? G[i] : 0.0;  // row / column 12 of G carries dv' C^: not part of Guu
+            Li[i] = (r == lc) ? 1.0 : 0.0;
+            X[i] = (i < 3) ? bt[i < 3 ? i : 0] : 0.0;
         }
-        // Leg blocks with T = 0 (swing legs; apex legs in the polish) have Guu block = I and no
-        // coupling (their Bt columns and off-diagonal Rr are exactly zero): their elimination step
-        // is the identity and is skipped.  amask is wave-uniform (scalar branches).
         int amask;
         {
             amask = (ag[0] != 0.0 ? 1 : 0) | (ag[1] != 0.0 ? 2 : 0) | (ag[2] != 0.0 ? 4 : 0) | (ag[3] != 0.0 ? 8 : 0);
             amask = __builtin_amdgcn_readfirstlane(amask);
         }
-        if (amask) {  // pivot columns of the first coupled block
-            const int b0 = __builtin_ctz(amask);
-            if (lane >= 3 * b0 && lane < 3 * b0 + 3) {
-#pragma unroll
-                for (int r = 0; r < 12; ++r) S.PNL[(lane - 3 * b0) * 12 + r] = a[r];
-            }
-        }
-        int par = 0;  // PNL buffer in use (double-buffered: the next block publishes while this one is read)
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
             if (!((amask >> blk) & 1)) continue;
             const int o = 3 * blk;
-            const ldouble* pnl = S.PNL + par * 36;
+            const int i0 = o >> 2, i1 = (o + 2) >> 2;  // registers holding rows o..o+2 (static)
+            const int ra = 4 * i0 + lr - o, rb = 4 * i1 + lr - o;
+            const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
             LMPC_SYNC();
-            const double i00 = rsq_nr(pnl[o]);
-            const double l10 = pnl[o + 1] * i00, l20 = pnl[o + 2] * i00;
-            const double i11 = rsq_nr(pnl[12 + o + 1] - l10 * l10);
-            const double l21 = (pnl[12 + o + 2] - l20 * l10) * i11;
-            const double i22 = rsq_nr(pnl[24 + o + 2] - l20 * l20 - l21 * l21);
-            const double z0 = i00 * a[o];
-            const double z1 = (a[o + 1] - l10 * z0) * i11;
-            const double z2 = (a[o + 2] - l20 * z0 - l21 * z1) * i22;
-            const int rest = amask >> (blk + 1);  // coupled blocks still to come
-            if (blk < 3 && rest) {
-                const double y2 = z2 * i22;
-                const double y1 = (z1 - l21 * y2) * i11;
-                const double y0 = (z0 - l10 * y1 - l20 * y2) * i00;
-                const int nb = blk + 1 + __builtin_ctz(rest);
-                // the next coupled block's rows first, then publish its pivot columns, then the rest
-#pragma unroll
-                for (int r = o + 3; r < o + 6; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
-                const bool pub = lane >= 3 * nb && lane < 3 * nb + 3;
-                ldouble* nx = S.PNL + (par ^ 1) * 36 + (pub ? (lane - 3 * nb) * 12 : 0);
-                if (pub && nb == blk + 1) {
-#pragma unroll
-                    for (int r = o + 3; r < o + 6; ++r) nx[r] = a[r];
-                }
-#pragma unroll
-                for (int r = o + 6; r < 12; ++r) a[r] -= pnl[r] * y0 + pnl[12 + r] * y1 + pnl[24 + r] * y2;
-                if (pub) {
-#pragma unroll
-                    for (int r = o + 6; r < 12; ++r) nx[r] = a[r];
+            {
+                ldouble* da = ina ? pv + 16 * ra + lc : sink + lane;
+                da[0] = Tg[i0];
+                if (i1 != i0) {
+                    ldouble* db = inb ? pv + 16 * rb + lc : sink + lane;
+                    db[0] = Tg[i1];
                 }
             }
-            a[o] = z0;
-            a[o + 1] = z1;
-            a[o + 2] = z2;
-            par ^= 1;
+            LMPC_SYNC();
+            const double p00 = pv[o], p10 = pv[16 + o], p11 = pv[16 + o + 1];
+            const double p20 = pv[32 + o], p21 = pv[32 + o + 1], p22 = pv[32 + o + 2];
+            const double t0 = pv[lc], t1 = pv[16 + lc], t2 = pv[32 + lc];  // Guu[o+a][lc] = Guu[lc][o+a]
+            {
+                ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + lane;
+                da[0] = Li[i0];
+                ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + lane;
+                dx[0] = X[i0];
+                Li[i0] = ina ? 0.0 : Li[i0];
+                X[i0] = ina ? 0.0 : X[i0];
+                if (i1 != i0) {
+                    ldouble* db = inb ? pv + 48 + 16 * rb + lc : sink + lane;
+                    db[0] = Li[i1];
+                    ldouble* dy = inb ? pv + 96 + 16 * rb + lc : sink + lane;
+                    dy[0] = X[i1];
+                    Li[i1] = inb ? 0.0 : Li[i1];
+                    X[i1] = inb ? 0.0 : X[i1];
+                }
+            }
+            LMPC_SYNC();
+            const double w0 = pv[48 + lc], w1 = pv[64 + lc], w2 = pv[80 + lc];
+            const double y0 = pv[96 + lc], y1 = pv[112 + lc], y2 = pv[128 + lc];
+            const double i00 = rsq_nr(p00);
+            const double l10 = p10 * i00, l20 = p20 * i00;
+            const double i11 = rsq_nr(fma(-l10, l10, p11));
+            const double l21 = fma(-l20, l10, p21) * i11;
+            const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
+            // row lc of L_C (zero in and above the pivot rows)
+            const double x0 = t0 * i00;
+            const double x1 = fma(-l10, x0, t1) * i11;
+            const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
+            const double xs = lr == 0 ? x0 : lr == 1 ? x1 : x2;
+            const double av = (lc > o + 2 && lr < 3) ? xs : 0.0;
+            // column lc of L_p^-1 W_p and of L_p^-1 X_p
+            const double v0 = w0 * i00;
+            const double v1 = fma(-l10, v0, w1) * i11;
+            const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
+            const double q0 = y0 * i00;
+            const double q1 = fma(-l10, q0, y1) * i11;
+            const double q2 = fma(-l21, q1, fma(-l20, q0, y2)) * i22;
+            const double bw = lr == 0 ? v0 : lr == 1 ? v1 : lr == 2 ? v2 : 0.0;
+            const double bx = lr == 0 ? q0 : lr == 1 ? q1 : lr == 2 ? q2 : 0.0;
+            const bool cp = lc >= o && lc <= o + 2;
+            const double aw = cp ? (lr == lc - o ? 1.0 : 0.0) : -av;
+            Tg = MFMA64(-av, av, Tg);
+            Li = MFMA64(aw, bw, Li);
+            X = MFMA64(aw, bx, X);
             SUB(9 + blk);
         }
-        // out, branch-free: lanes 12-17 -> V (global, and LDS for K^), lanes 18-29 -> packed L^-1
-        // (global); upper-triangle entries and idle lanes go to dummy words
+        // factor outputs: V (columns 6-11 of V^) and packed L^-1 to the global scratch (branch-free)
 #pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            g[oofs[r]] = a[r];
-            vl[r * vstep] = a[r];
+        for (int i = 0; i < 3; ++i) {
+            g[vofs[i]] = X[i];
+            g[lofs[i]] = Li[i];
         }
-        LMPC_SYNC();
         SUB(7);
-        // ---- K^ = V^' V^ (V^ = [0 | V], columns 6-11) ----
+        // ---- K^ = V^' V^ (V^ = [0 | V], columns 6-11; rows 0-11 = k-blocks 0-2) ----
         d4 KH = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int kk = 0; kk < 3; ++kk) {
-            const double vh = vop[4 * kk];
-            KH = MFMA64(vh, vh, KH);
-        }
+        for (int kk = 0; kk < 3; ++kk) KH = MFMA64(X[kk], X[kk], KH);
         // ---- KZ^ = K^ PA (k-blocks 1-2: K^ is zero outside rows/columns 6-11) ----
         d4 KZ = {0.0, 0.0, 0.0, 0.0};
         KZ = MFMA64(KH[1], PA[1], KZ);
