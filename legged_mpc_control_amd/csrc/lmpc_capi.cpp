@@ -191,6 +191,8 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
         c->prm.gi_max_steps = gm ? std::atoi(gm) : 240;
         const char* dc = std::getenv("LMPC_DENSE_ITER_CAP");  // test hook: the interior point's hand-over
         c->prm.dense_iter_cap = dc ? std::atoi(dc) : (1 << 30);
+        const char* dp = std::getenv("LMPC_DENSE_POLISH_ITER");  // tuning hook (tools/)
+        c->prm.dense_polish_iter = dp ? std::atoi(dp) : LMPC_DENSE_POLISH_ITER;
         const char* wr = std::getenv("LMPC_WARM_ROUNDS");  // tuning hook (tools/)
         c->prm.warm_rounds = wr ? std::atoi(wr) : 12;  // tools/tick_latency sweep: 4 -> 0.59 ms, 12 -> 0.35 ms at H=30
     }

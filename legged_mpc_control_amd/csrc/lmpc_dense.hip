@@ -114,7 +114,9 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
     enum { PRED = 0, CORR = 1, POLISH = 2 };
     const double mc = 5.0 * nls;
     double tol = prm.tol_mu;
-    int att = 0, rd = 0, it_end = prm.max_iter, mode = PRED, act = 0;
+    // first attempt: at most dense_polish_iter interior-point iterations before the polish (the polish verifies
+    // the optimum exactly; a failed polish resumes the interior point with a tighter tolerance below)
+    int att = 0, rd = 0, it_end = min(prm.max_iter, prm.dense_polish_iter), mode = PRED, act = 0;
     bool apex = false;
     double mu_c = 0.0, smu = 0.0;
     // factor tiles (register resident through the corrector): U's off-diagonal tiles in Tl, U_bb^-1, U_bb^-T

@@ -25,6 +25,7 @@ struct DevParams {
     int dense;         // QPs with 1..DENSE_MAX_LS stance leg-steps: 0 Riccati kernel, 1 condensed interior
                        // point (lmpc_dense.hip), 2 condensed dual active set (lmpc_gi.hip)
     int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel
+    int dense_polish_iter;  // condensed interior point: iterations of the first attempt before the active-set polish
     int dense_iter_cap;  // condensed interior point: IPM iterations after which a QP is handed to the Riccati
                          // kernel (test hook LMPC_DENSE_ITER_CAP; default: never, max_iter governs)
     int cus;           // compute units of the device (launch shaping only)
@@ -36,6 +37,9 @@ struct DevParams {
     uint8_t* act_out;
     int warm_rounds;   // polish rounds a warm start may take before the cold fallback
 };
+#ifndef LMPC_DENSE_POLISH_ITER
+#define LMPC_DENSE_POLISH_ITER 40  // = lmpc_options_default max_iter: the polish only once the IPM has converged
+#endif
 constexpr int DENSE_MAX_LS = 20;  // 5 leg-steps per 16-wide tile x 4 tiles (lmpc_dense.hip)
 constexpr int DENSE_MAX_H = 16;   // the dense path's per-step LDS arrays
 

@@ -29,7 +29,7 @@ def leg_cons(mu, fmax):
     return C, c0
 
 
-def gi(Hm, g, nls, mu, fmax, stats):
+def gi(Hm, g, nls, mu, fmax, stats, max_steps=None):
     n = Hm.shape[0]
     Cl, c0l = leg_cons(mu, fmax)
     m = 5 * nls
@@ -53,6 +53,8 @@ def gi(Hm, g, nls, mu, fmax, stats):
         if not s[p] < -tol:
             break
         sp = s[p]
+        if max_steps is not None and it >= max_steps:  # truncated run (tools/hybrid_proto.py): stop at an add
+            break
         q = len(act)
         uu = np.append(lam[act], 0.0)
         stats["adds"] += 1
@@ -121,6 +123,7 @@ def gi(Hm, g, nls, mu, fmax, stats):
             sp = sval(p)
     stats["iters"] = it
     stats["nact"] = len(act)
+    stats["active"] = list(act)
     return x
 
 
