@@ -4,7 +4,8 @@ active-face bitmask, the leg's null-space basis T / particular solution up, T'HT
 added (most violated) or dropped (most negative multiplier) per leg-step per round), driven from different
 starting guesses, to price strategies for the B = 1024 tail before touching the kernel:
   ipm:K   -- K Mehrotra iterations (or to tol_mu) then the polish from z > s (the kernel's rule);
-  gi:K    -- K dual active-set steps then the polish from the GI working set.
+  gi:K    -- K dual active-set steps then the polish from the GI working set;
+  a third field picks the polish update: single (the kernel's, default) or pdas (primal-dual active set).
 Cost model in cycles per QP from the v15 stamps: IPM iteration 55 k, polish round 45 k,
 GI step 10.5 k, GI start (Cholesky + J) 45 k, prologue + condensation 55 k."""
 import os
@@ -50,7 +51,7 @@ def drop_face(act, g, mu, zmin):
     return rows[k] if z[k] < zmin else -1
 
 
-def polish(Hm, g, act, mu, fmax, max_rounds=12, tol_p=1e-9, tol_d=1e-9):
+def polish(Hm, g, act, mu, fmax, max_rounds=12, tol_p=1e-9, tol_d=1e-9, rule="single"):
     nls = len(act)
     act = list(act)
     for rd in range(1, max_rounds + 1):
@@ -76,6 +77,27 @@ def polish(Hm, g, act, mu, fmax, max_rounds=12, tol_p=1e-9, tol_d=1e-9):
         for b in range(nls):
             o = C @ u[3 * b:3 * b + 3] - bb
             gl = grad[3 * b:3 * b + 3]
+            if rule == "pdas" and not apex[b]:
+                # primal-dual active set: every violated face in, every face with a negative multiplier out
+                rows = [i for i in range(5) if (act[b] >> i) & 1][:3]
+                lam = np.zeros(5)
+                if rows:
+                    lam[rows] = np.linalg.lstsq(C[rows].T, -gl, rcond=None)[0]
+                score = np.where([(act[b] >> i) & 1 for i in range(5)], lam, -(-o))  # active: lambda; inactive: violation
+                new = 0
+                order = np.argsort(-score)
+                for i in order:
+                    isact = (act[b] >> i) & 1
+                    keep = (isact and lam[i] >= -tol_d * gscale) or (not isact and o[i] > tol_p * fmax)
+                    if keep and bin(new).count("1") < 3:
+                        cand = new | (1 << int(i))
+                        if np.linalg.matrix_rank(C[[k for k in range(5) if (cand >> k) & 1]]) == bin(cand).count("1") \
+                                or (cand & 3) == 3 or (cand & 12) == 12:
+                            new = cand
+                if new != act[b]:
+                    act[b] = new
+                    changed = True
+                continue
             cand = [(o[i], i) for i in range(5) if not (act[b] >> i) & 1 and o[i] > tol_p * fmax]
             if cand:
                 act[b] |= 1 << max(cand)[1]
@@ -187,8 +209,9 @@ def main():
         ref, _, _ = O.solve(op, H, rec[b], con[b])
         data.append((Hm, g, st, idx, ref))
     for spec in strategies:
-        kind, K = spec.split(":")
-        K = int(K)
+        parts = spec.split(":")
+        kind, K = parts[0], int(parts[1])
+        rule = parts[2] if len(parts) > 2 else "single"
         costs, rounds, fails, err = [], [], 0, 0.0
         for Hm, g, st, idx, ref in data:
             if kind == "ipm":
@@ -197,7 +220,7 @@ def main():
             else:
                 act, it = gi_then_act(Hm, g, len(st), p, K)
                 cost = 55e3 + 45e3 + it * 10.5e3
-            u, rd, ok = polish(Hm, g, act, p.mu, p.f_max)
+            u, rd, ok = polish(Hm, g, act, p.mu, p.f_max, rule=rule)
             fails += not ok
             cost += rd * 45e3
             costs.append(cost)
