@@ -37,6 +37,13 @@ EXPORTED_SYMBOLS = (
     "lmpc_set_dense_path", "lmpc_get_dense_path",
 )
 ABI_VERSION = 4
+# include/lmpc/lmpc_hoqp.h: batched hierarchical QP (whole-body control)
+HOQP_SYMBOLS = (
+    "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
+    "lmpc_hoqp_create", "lmpc_hoqp_destroy", "lmpc_hoqp_set_options", "lmpc_hoqp_solve_batch",
+    "lmpc_hoqp_solve_device", "lmpc_hoqp_sync",
+)
+HOQP_MAX_LEVELS = 4
 
 
 class LmpcParams(ctypes.Structure):
@@ -105,6 +112,19 @@ class LmpcLegKin(ctypes.Structure):
         ("rho_fix", (ctypes.c_double * 5) * 4),
         ("rho_opt", (ctypes.c_double * 3) * 4),
     ]
+
+
+class LmpcHoqpDims(ctypes.Structure):
+    _fields_ = [
+        ("num_vars", ctypes.c_int32),
+        ("num_levels", ctypes.c_int32),
+        ("eq_rows", ctypes.c_int32 * HOQP_MAX_LEVELS),
+        ("ineq_rows", ctypes.c_int32 * HOQP_MAX_LEVELS),
+    ]
+
+
+class LmpcHoqpOptions(ctypes.Structure):
+    _fields_ = [("max_iter", ctypes.c_int32), ("tol_mu", ctypes.c_double), ("tol_res", ctypes.c_double)]
 
 
 class NativeLibraryError(RuntimeError):
@@ -205,6 +225,27 @@ def lib():
         L.lmpc_grf_to_torque.restype = ctypes.c_int
         L.lmpc_grf_to_torque_device.argtypes = [vp, kp, vp, vp, vp, ctypes.c_int, vp, vp]
         L.lmpc_grf_to_torque_device.restype = ctypes.c_int
+        hdp, hop = ctypes.POINTER(LmpcHoqpDims), ctypes.POINTER(LmpcHoqpOptions)
+        L.lmpc_hoqp_dims_wbc.argtypes = [hdp]
+        L.lmpc_hoqp_dims_wbc.restype = None
+        L.lmpc_hoqp_options_default.argtypes = [hop]
+        L.lmpc_hoqp_options_default.restype = None
+        L.lmpc_hoqp_record_len.argtypes = [hdp]
+        L.lmpc_hoqp_record_len.restype = ctypes.c_int64
+        L.lmpc_hoqp_slack_len.argtypes = [hdp]
+        L.lmpc_hoqp_slack_len.restype = ctypes.c_int
+        L.lmpc_hoqp_create.argtypes = [hdp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.lmpc_hoqp_create.restype = ctypes.c_int
+        L.lmpc_hoqp_destroy.argtypes = [vp]
+        L.lmpc_hoqp_destroy.restype = None
+        L.lmpc_hoqp_set_options.argtypes = [vp, hop]
+        L.lmpc_hoqp_set_options.restype = ctypes.c_int
+        L.lmpc_hoqp_solve_batch.argtypes = [vp, dp, ctypes.c_int, dp, dp, i32p, i32p]
+        L.lmpc_hoqp_solve_batch.restype = ctypes.c_int
+        L.lmpc_hoqp_solve_device.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, vp, vp]
+        L.lmpc_hoqp_solve_device.restype = ctypes.c_int
+        L.lmpc_hoqp_sync.argtypes = [vp]
+        L.lmpc_hoqp_sync.restype = ctypes.c_int
         if L.lmpc_abi_version() != ABI_VERSION:
             raise NativeLibraryError("liblmpc.so ABI version mismatch")
         _lib = L

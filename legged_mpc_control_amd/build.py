@@ -16,8 +16,9 @@ ARCH = "gfx950"
 # config 2 0.342 -> 0.329 ms, config 4 22.4 -> 22.0 ms (profiles/r02/diag_ab_configs.log).
 HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 
-SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
-HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h"]
+SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_capi.cpp",
+           "hoqp_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
+HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_hoqp_device.h"]
 
 
 def hipcc() -> str:
@@ -37,7 +38,8 @@ def _stale(target: str, deps) -> bool:
 def build_native(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [
-        os.path.join(ROOT, "include", "lmpc", "lmpc.h"), os.path.join(ROOT, "include", "lmpc", "ConvexQPSolver.hpp"),
+        os.path.join(ROOT, "include", "lmpc", "lmpc.h"), os.path.join(ROOT, "include", "lmpc", "lmpc_hoqp.h"),
+        os.path.join(ROOT, "include", "lmpc", "ConvexQPSolver.hpp"),
         os.path.abspath(__file__)]
     if not force and not _stale(LIB, deps):
         return LIB

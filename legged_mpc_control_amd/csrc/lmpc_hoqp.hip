@@ -1,0 +1,697 @@
+// lmpc_hoqp.hip -- batched hierarchical QP of the whole-body controller, one wavefront
+// per instance, all levels in one launch.
+//
+// Reference: src/legged_ctrl/src/wbc_ctrl/HoQp.cpp (one qpOASES QProblem per priority level) and
+// include/wbc_ctrl/task.h; caller wbc.cpp:93-99.  Per level l, with Z the null-space basis of every higher
+// level's equalities (n x nd, identity at level 0) and x the higher levels' solution:
+//   setup   G = A_l Z (m x nd) and the level gradient c = G'(A_l x - b_l)            (HoQp.cpp:94-107)
+//           Hy = G'G + 1e-12 I                                                         (:73-92)
+//           Z' = Z ker(G), ker from Eigen's FullPivLU (full pivoting, rank threshold
+//           eps * min(m, nd) * max pivot, basis Q [-U11^-1 U12; I])                    (:147-156)
+//           constraint rows in y: R = [D_stack Z; D_l Z], bounds h = f_stack - D_stack x + w_stack,
+//           g = f_l - D_l x, the stacked rows current-first and the slacks current-last, as the
+//           reference pairs them                                                      (:58, :109-145, :176-182)
+//   solve   min 1/2 y'Hy y + c'y + 1/2 |v|^2  s.t. -v <= 0, D_stack Z y <= h, D_l Z y - v <= g   (:158-174)
+//           by a Mehrotra interior point over (y, v) with v eliminated: per iteration
+//           K = Hy + R' diag(w) R (w = z/s on frozen rows, w3 (1 + w1)/(1 + w1 + w3) on own rows) on the
+//           matrix cores, its Cholesky factor with a pivot floor (Hy is singular in double along ker G,
+//           where 1e-12 is below the rounding of G'G: such a pivot freezes its coordinate), two solves;
+//           afterwards v = max(0, D_l Z y - g) exactly for the final y
+//   output  x += Z y (HoQp.h:41-45), w_l = v, and Z <- Z'.
+// Layout: the instance records stay in HBM and are read by the level setup only; the level's constraint
+// rows R and K live in LDS (one wave = one instance, ~40 KB at the WBC's n = 42); Z, Z' and Hy live in a
+// per-instance global scratch (L2-resident), read once per level or once per iteration.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "lmpc_hoqp_device.h"
+#include "lmpc_kernel_common.h"
+
+namespace lmpc {
+namespace {
+
+constexpr double HQ_REG = 1e-12;        // HoQp.cpp:84
+constexpr double HQ_PIV_FLOOR = 1e-13;  // relative to max(1, largest diagonal entry of K)
+constexpr double HQ_PIV_BIG = 1e64;     // pivot of a frozen coordinate
+constexpr double HQ_FRAC = 0.99;        // fraction of the step to the boundary
+
+typedef __attribute__((address_space(3))) int lint;
+
+struct HS {
+    ldouble* R;    // rmax x ls: constraint rows in y (columns nd..np-1 zero)
+    ldouble* KL;   // kmax x ls: G (setup, FullPivLU) then K and its Cholesky factor (lower)
+    ldouble* y;    // np
+    ldouble* dy;   // np
+    ldouble* c;    // np: level gradient
+    ldouble* x;    // np: x (n used)
+    ldouble* dI;   // np: 1 / L_kk
+    ldouble* vb;   // kmax: A x - b during setup
+    ldouble* q;    // rmax: per-row operand of R' q
+    ldouble* wh;   // rmax: per-row weight of K
+    ldouble* t;    // rmax: spare per-row vector
+    lint* rt;      // 64: FullPivLU row transpositions
+    lint* ct;      // 64: column transpositions
+    lint* qp;      // 64: column permutation Q
+    lint* pv;      // 64: pivots above the rank threshold
+};
+
+__device__ __forceinline__ HS carve(ldouble* sm, const HoqpDev& P) {
+    HS S;
+    const int ls = hq_ls(P);
+    S.R = sm;
+    S.KL = S.R + (size_t)P.rmax * ls;
+    S.y = S.KL + (size_t)P.kmax * ls;
+    S.dy = S.y + P.np;
+    S.c = S.dy + P.np;
+    S.x = S.c + P.np;
+    S.dI = S.x + P.np;
+    S.vb = S.dI + P.np;
+    S.q = S.vb + P.kmax;
+    S.wh = S.q + P.rmax;
+    S.t = S.wh + P.rmax;
+    S.rt = (lint*)(S.t + P.rmax);
+    S.ct = S.rt + 64;
+    S.qp = S.ct + 64;
+    S.pv = S.qp + 64;
+    return S;
+}
+
+// level l's blocks inside one record
+__device__ __forceinline__ const double* lev_a(const HoqpDev& P, const double* rec, int l) { return rec + P.off[l]; }
+__device__ __forceinline__ const double* lev_b(const HoqpDev& P, const double* rec, int l) {
+    return rec + P.off[l] + (int64_t)P.m[l] * P.n;
+}
+__device__ __forceinline__ const double* lev_d(const HoqpDev& P, const double* rec, int l) {
+    return rec + P.off[l] + (int64_t)P.m[l] * (P.n + 1);
+}
+__device__ __forceinline__ const double* lev_f(const HoqpDev& P, const double* rec, int l) {
+    return lev_d(P, rec, l) + (int64_t)P.s[l] * P.n;
+}
+
+// Row r of level l's constraint block: r < p = sum_{k<l} s_k are the higher levels' rows stacked
+// current-first, [d_{l-1}; d_{l-2}; ...; d_0] (stacked_tasks_ = task_ + stacked_tasks_prev_, HoQp.cpp:58);
+// r >= p is the level's own row r - p.  Returns the row and its f.
+__device__ __forceinline__ const double* cons_row(const HoqpDev& P, const double* rec, int l, int p, int r,
+                                                  double& f) {
+    int lev = l, idx = r - p;
+    if (r < p) {
+        idx = r;
+        for (int k = l - 1; k >= 0; --k) {
+            if (idx < P.s[k]) {
+                lev = k;
+                break;
+            }
+            idx -= P.s[k];
+        }
+    }
+    f = lev_f(P, rec, lev)[idx];
+    return lev_d(P, rec, lev) + (int64_t)idx * P.n;
+}
+
+// C[rows][0..np) = X Z on the matrix cores; X row r = xrow(r) (global, n entries), Z global n x np
+// (columns nd..np-1 zero).  A[m][k] comes from lane 16k+m, B[k][n] from lane 16k+n, C element (4i+g, c)
+// lands in register i of lane 16g+c.
+template <class RowFn>
+__device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, const gdouble* Z, ldouble* C, int ldc, int lane) {
+    const int kq = lane >> 4, mm = lane & 15;
+    for (int I = 0; I * 16 < rows; ++I) {
+        const double* xr = (16 * I + mm < rows) ? xrow(16 * I + mm) : nullptr;
+        d4 acc[4];
+#pragma unroll
+        for (int J = 0; J < 4; ++J) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < P.n; k0 += 4) {
+            const int k = k0 + kq;
+            const double a = (xr != nullptr && k < P.n) ? xr[k] : 0.0;
+#pragma unroll
+            for (int J = 0; J < 4; ++J)
+                if (J < P.nt) {
+                    const double bz = k < P.n ? Z[(int64_t)k * P.np + 16 * J + mm] : 0.0;
+                    acc[J] = MFMA64(a, bz, acc[J]);
+                }
+        }
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+            if (J < P.nt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * I + 4 * i + kq;
+                    if (row < rows) C[row * ldc + 16 * J + mm] = acc[J][i];
+                }
+            }
+    }
+}
+
+// Lower tiles (I >= J) of sum_r w_r M[r][.]' M[r][.] over rows 0..rows-1 of an LDS matrix (stride ld,
+// np columns), accumulated onto acc[tile(I,J)] (w == nullptr: unit weights).
+__device__ __forceinline__ int tid(int I, int J) { return I * (I + 1) / 2 + J; }
+__device__ __forceinline__ void sym_tiles(const HoqpDev& P, const ldouble* M, int ld, int rows, const ldouble* w, d4 acc[10],
+                          int lane) {
+    const int kq = lane >> 4, mm = lane & 15;
+    for (int r0 = 0; r0 < rows; r0 += 4) {
+        const int r = r0 + kq;
+        const bool live = r < rows;
+        const double wr = live ? (w ? w[r] : 1.0) : 0.0;
+        double v[4];
+#pragma unroll
+        for (int I = 0; I < 4; ++I) v[I] = (live && I < P.nt) ? M[r * ld + 16 * I + mm] : 0.0;
+#pragma unroll
+        for (int I = 0; I < 4; ++I)
+            if (I < P.nt) {
+                const double a = wr * v[I];
+#pragma unroll
+                for (int J = 0; J <= I; ++J) acc[tid(I, J)] = MFMA64(a, v[J], acc[tid(I, J)]);
+            }
+    }
+}
+
+// Cholesky factor of K (nd x nd, lower, in place, row-parallel: lane i = row i) with a pivot floor;
+// dI[k] = 1 / L_kk.
+__device__ void chol_floor(const HS& S, int ls, int nd, int lane) {
+    double dmax = lane < nd ? S.KL[lane * ls + lane] : 0.0;
+    dmax = wave_max(dmax);
+    const double thr = HQ_PIV_FLOOR * fmax(1.0, dmax);
+    for (int k = 0; k < nd; ++k) {
+        const double pkk = S.KL[k * ls + k];
+        const double piv = pkk > thr ? pkk : HQ_PIV_BIG;
+        const double inv = 1.0 / sqrt(piv);
+        LMPC_SYNC();
+        double l = 0.0;
+        if (lane == k) {
+            S.KL[k * ls + k] = piv * inv;
+            S.dI[k] = inv;
+        } else if (lane > k && lane < nd) {
+            l = S.KL[lane * ls + k] * inv;
+            S.KL[lane * ls + k] = l;
+        }
+        LMPC_SYNC();
+        if (lane > k && lane < nd)
+            for (int j = k + 1; j <= lane; ++j) S.KL[lane * ls + j] -= l * S.KL[j * ls + k];
+        LMPC_SYNC();
+    }
+}
+
+// K u = rhs with K = L L': rhs in lane i (i < nd); returns u in lane i, also stored to out[i].
+__device__ double chol_solve(const HS& S, int ls, int nd, double rhs, ldouble* out, int lane) {
+    const double di = lane < nd ? S.dI[lane] : 0.0;
+    double acc = lane < nd ? rhs : 0.0;
+    double u = 0.0;
+    for (int k = 0; k < nd; ++k) {  // L w = rhs
+        const double lik = (lane > k && lane < nd) ? S.KL[lane * ls + k] : 0.0;
+        const double wk = readlane_f64(acc * di, k);
+        if (lane == k) u = wk;
+        acc = fma(-lik, wk, acc);
+    }
+    acc = u;
+    double sol = 0.0;
+    for (int k = nd - 1; k >= 0; --k) {  // L' u = w
+        const double lki = lane < k ? S.KL[k * ls + lane] : 0.0;
+        const double xk = readlane_f64(acc * di, k);
+        if (lane == k) sol = xk;
+        acc = fma(-lki, xk, acc);
+    }
+    if (lane < nd) out[lane] = sol;
+    LMPC_SYNC();
+    return sol;
+}
+
+// t = R_r . vec (row r, nd columns)
+__device__ __forceinline__ double row_dot(const HS& S, int ls, int nd, int r, const ldouble* vec) {
+    double a = 0.0;
+    for (int j = 0; j < nd; ++j) a = fma(S.R[r * ls + j], vec[j], a);
+    return a;
+}
+// (R' q)_j for lane j
+__device__ __forceinline__ double rt_dot(const HS& S, int ls, int nr, const ldouble* q, int lane) {
+    double a = 0.0;
+    for (int r = 0; r < nr; ++r) a = fma(S.R[r * ls + lane], q[r], a);
+    return a;
+}
+
+// Eigen FullPivLU of G (m x nd in S.KL) and Z' = Z ker(G) into Zn (n x np); returns the new nd.
+// Restates Eigen/src/LU/FullPivLU.h (3.3): compute() and kernel_retval::evalTo (tests/test_hoqp_oracle.py
+// pins the CPU restatement, oracle/hoqp.py fullpivlu / fullpivlu_kernel, that this follows step by step).
+__device__ int fullpivlu_kernel(const HoqpDev& P, const HS& S, int m, int nd, const gdouble* Z, gdouble* Zn,
+                                int lane) {
+    const int ls = hq_ls(P);
+    const int size = m < nd ? m : nd;
+    int nonzero = size;
+    double maxpiv = 0.0;
+    if (lane < 64) {
+        S.rt[lane] = lane;
+        S.ct[lane] = lane;
+    }
+    LMPC_SYNC();
+    for (int k = 0; k < size; ++k) {
+        // largest |G_ij| over i >= k, j >= k; the first in column-major order wins a tie (maxCoeff)
+        double best = -1.0;
+        int brow = k;
+        if (lane >= k && lane < nd)
+            for (int i = k; i < m; ++i) {
+                const double a = fabs(S.KL[i * ls + lane]);
+                if (a > best) {
+                    best = a;
+                    brow = i;
+                }
+            }
+        const double wbest = wave_max(best);
+        if (wbest == 0.0) {
+            nonzero = k;
+            break;
+        }
+        const unsigned long long hit = __ballot(best == wbest && lane >= k && lane < nd);
+        const int c = __ffsll((long long)hit) - 1;
+        const int r = __builtin_amdgcn_readlane(brow, c);
+        maxpiv = fmax(maxpiv, wbest);
+        if (lane == 0) {
+            S.rt[k] = r;
+            S.ct[k] = c;
+        }
+        if (r != k && lane < nd) {  // swap rows k, r
+            const double a = S.KL[k * ls + lane], b = S.KL[r * ls + lane];
+            S.KL[k * ls + lane] = b;
+            S.KL[r * ls + lane] = a;
+        }
+        LMPC_SYNC();
+        if (c != k && lane < m) {  // swap columns k, c
+            const double a = S.KL[lane * ls + k], b = S.KL[lane * ls + c];
+            S.KL[lane * ls + k] = b;
+            S.KL[lane * ls + c] = a;
+        }
+        LMPC_SYNC();
+        const double pk = S.KL[k * ls + k];
+        if (lane > k && lane < m) {
+            const double l = S.KL[lane * ls + k] / pk;
+            S.KL[lane * ls + k] = l;
+            for (int j = k + 1; j < nd; ++j) S.KL[lane * ls + j] -= l * S.KL[k * ls + j];
+        }
+        LMPC_SYNC();
+    }
+    // permutation Q from the column transpositions, applied in increasing k (m_q)
+    if (lane == 0) {
+        for (int j = 0; j < nd; ++j) S.qp[j] = j;
+        for (int k = 0; k < size; ++k) {
+            const int a = S.qp[k], b = S.qp[S.ct[k]];
+            S.qp[k] = b;
+            S.qp[S.ct[k]] = a;
+        }
+    }
+    // rank: pivots above eps * diagonalSize * maxpivot (rank(), kernel())
+    const double thr = maxpiv * (DBL_EPSILON * (double)size);
+    int rank = 0;
+    if (lane == 0)
+        for (int i = 0; i < nonzero; ++i)
+            if (fabs(S.KL[i * ls + i]) > thr) S.pv[rank++] = i;
+    rank = __builtin_amdgcn_readfirstlane(rank);
+    LMPC_SYNC();
+    const int dimker = nd - rank;
+    if (dimker == 0) {  // trivial kernel: Eigen returns one zero column
+        for (int j = 0; j < P.np; ++j)
+            if (lane < P.n) Zn[(int64_t)lane * P.np + j] = 0.0;
+        return 1;
+    }
+    // trapezoid m (rank x nd) in place: row i <- U row pv[i] from column i on, head zero
+    for (int i = 0; i < rank; ++i) {
+        const int src = S.pv[i];
+        double v = 0.0;
+        if (lane < nd && lane >= i) v = S.KL[src * ls + lane];
+        LMPC_SYNC();
+        if (lane < nd) S.KL[i * ls + lane] = v;
+        LMPC_SYNC();
+    }
+    // bring the non-negligible pivots onto the diagonal (column swaps), solve U11 M = U12, swap back
+    for (int i = 0; i < rank; ++i) {
+        const int pc = S.pv[i];
+        if (pc != i && lane < rank) {
+            const double a = S.KL[lane * ls + i], b = S.KL[lane * ls + pc];
+            S.KL[lane * ls + i] = b;
+            S.KL[lane * ls + pc] = a;
+        }
+        LMPC_SYNC();
+    }
+    if (lane < dimker) {  // back substitution, one right-hand side per lane
+        const int col = rank + lane;
+        for (int i = rank - 1; i >= 0; --i) {
+            double a = S.KL[i * ls + col];
+            for (int j = i + 1; j < rank; ++j) a -= S.KL[i * ls + j] * S.KL[j * ls + col];
+            S.KL[i * ls + col] = a / S.KL[i * ls + i];
+        }
+    }
+    LMPC_SYNC();
+    for (int i = rank - 1; i >= 0; --i) {
+        const int pc = S.pv[i];
+        if (pc != i && lane < rank) {
+            const double a = S.KL[lane * ls + i], b = S.KL[lane * ls + pc];
+            S.KL[lane * ls + i] = b;
+            S.KL[lane * ls + pc] = a;
+        }
+        LMPC_SYNC();
+    }
+    // basis K: row Q[i] = -M[i] (i < rank), row Q[rank + k] = e_k;  Z' = Z K, lane = row of Z
+    if (lane < P.n) {
+        const gdouble* zr = Z + (int64_t)lane * P.np;
+        for (int cc = 0; cc < P.np; ++cc) {
+            double a = 0.0;
+            if (cc < dimker) {
+                a = zr[S.qp[rank + cc]];
+                for (int i = 0; i < rank; ++i) a -= zr[S.qp[i]] * S.KL[i * ls + rank + cc];
+            }
+            Zn[(int64_t)lane * P.np + cc] = a;
+        }
+    }
+    return dimker;
+}
+
+// Interior-point state of the level's rows, slot k = row lane + 64 k (rows < nr = p + s, own rows r >= p).
+struct Rows {
+    double s1[2], z1[2], v[2];  // own rows: -v <= 0 with slack s1
+    double sg[2], zg[2];        // frozen rows: P y <= h; own rows: Dz y - v <= g
+    double bd[2];               // h or g
+};
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const double* __restrict__ recs,
+                                                       double* __restrict__ xout, double* __restrict__ wout,
+                                                       int32_t* __restrict__ status, int32_t* __restrict__ iters,
+                                                       double* __restrict__ scratch, int batch) {
+    extern __shared__ __attribute__((aligned(16))) double hq_smem[];
+    const int b = blockIdx.x;
+    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    const HS S = carve((ldouble*)hq_smem, P);
+    const int ls = hq_ls(P);
+    const double* rec = recs + (int64_t)b * P.rec_len;
+    gdouble* zbuf[2] = {(gdouble*)(scratch + (int64_t)b * P.scratch_len),
+                        (gdouble*)(scratch + (int64_t)b * P.scratch_len + (int64_t)P.n * P.np)};
+    gdouble* Hg = (gdouble*)(scratch + (int64_t)b * P.scratch_len + 2 * (int64_t)P.n * P.np);
+    gdouble* wo = (gdouble*)(wout + (int64_t)b * P.slack_len);
+    int zc = 0;
+    // Z = I, x = 0
+    if (lane < P.n)
+        for (int j = 0; j < P.np; ++j) zbuf[0][(int64_t)lane * P.np + j] = (j == lane) ? 1.0 : 0.0;
+    if (lane < P.np) S.x[lane] = 0.0;
+    LMPC_GSYNC();
+    int nd = P.n, p = 0, st = 0;
+    for (int l = 0; l < P.L; ++l) {
+        const int m = P.m[l], s = P.s[l], nr = p + s;
+        const gdouble* Z = zbuf[zc];
+        // ---- setup: G = A Z into KL, A x - b, c = G'(A x - b), Hy = G'G + 1e-12 I ---------------
+        if (lane < P.np) S.c[lane] = 0.0;
+        d4 acc[10];
+#pragma unroll
+        for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+        if (m > 0) {
+            const double* A = lev_a(P, rec, l);
+            gemm_xz(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, S.KL, ls, lane);
+            if (lane < m) {
+                const double* ar = A + (int64_t)lane * P.n;
+                double a = -lev_b(P, rec, l)[lane];
+                for (int k = 0; k < P.n; ++k) a = fma(ar[k], S.x[k], a);
+                S.vb[lane] = a;
+            }
+            LMPC_SYNC();
+            if (lane < nd) {
+                double a = 0.0;
+                for (int i = 0; i < m; ++i) a = fma(S.KL[i * ls + lane], S.vb[i], a);
+                S.c[lane] = a;
+            }
+            sym_tiles(P, S.KL, ls, m, nullptr, acc, lane);
+        }
+        {  // Hy to global, full symmetric, 1e-12 on the diagonal of the live block
+            const int g = lane >> 4, cc = lane & 15;
+#pragma unroll
+            for (int I = 0; I < 4; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J)
+                    if (I < P.nt) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int row = 16 * I + 4 * i + g, col = 16 * J + cc;
+                            double v = acc[tid(I, J)][i];
+                            if (row == col && row < nd) v += HQ_REG;
+                            Hg[(int64_t)row * P.np + col] = v;
+                            Hg[(int64_t)col * P.np + row] = v;
+                        }
+                    }
+        }
+        LMPC_GSYNC();
+        // ---- next basis Z' = Z ker(G) (HoQp.cpp:147-156), before K reuses the buffer ----------------
+        int nd_next = nd;
+        if (m > 0) nd_next = fullpivlu_kernel(P, S, m, nd, Z, zbuf[zc ^ 1], lane);
+        // ---- constraint rows R = [D_stack; D_l] Z and their bounds -----------------------------------
+        gemm_xz(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, ls, lane);
+        Rows W;
+        double bmax = 0.0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = lane + 64 * k;
+            W.s1[k] = W.z1[k] = 1.0;
+            W.v[k] = 0.0;
+            W.sg[k] = W.zg[k] = 1.0;
+            W.bd[k] = 0.0;
+            if (r < nr) {
+                double f;
+                const double* dr = cons_row(P, rec, l, p, r, f);
+                double a = f;
+                for (int j = 0; j < P.n; ++j) a = fma(-dr[j], S.x[j], a);
+                if (r < p) a += wo[r];  // frozen slack, stacked current-last (HoQp.cpp:141-142, :176-182)
+                W.bd[k] = a;
+                bmax = fmax(bmax, fabs(a));
+                if (r < p) {
+                    W.sg[k] = fmax(a, 1.0);
+                } else {
+                    W.v[k] = fmax(0.0, -a) + 1.0;
+                    W.s1[k] = fmax(W.v[k], 1.0);
+                    W.sg[k] = fmax(a + W.v[k], 1.0);
+                }
+            }
+        }
+        if (lane < P.np) {
+            S.y[lane] = 0.0;
+            S.dy[lane] = 0.0;
+        }
+        LMPC_SYNC();
+        const double scale = 1.0 + fmax(wave_max(lane < nd ? fabs(S.c[lane]) : 0.0), wave_max(bmax));
+        const double mc = (double)(p + 2 * s);
+        // ---- interior point --------------------------------------------------------------------------
+        int it = 0;
+        for (;; ++it) {
+            // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
+            double rp1[2], rpg[2], rdv[2];
+            double cs = 0.0, res = 0.0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                rp1[k] = rpg[k] = rdv[k] = 0.0;
+                if (r < nr) {
+                    const double ty = row_dot(S, ls, nd, r, S.y);
+                    S.q[r] = W.zg[k];
+                    if (r < p) {
+                        rpg[k] = ty + W.sg[k] - W.bd[k];
+                        cs += W.sg[k] * W.zg[k];
+                    } else {
+                        rpg[k] = ty - W.v[k] + W.sg[k] - W.bd[k];
+                        rp1[k] = -W.v[k] + W.s1[k];
+                        rdv[k] = W.v[k] - W.z1[k] - W.zg[k];
+                        cs += W.sg[k] * W.zg[k] + W.s1[k] * W.z1[k];
+                    }
+                    res = fmax(res, fmax(fabs(rpg[k]), fmax(fabs(rp1[k]), fabs(rdv[k]))));
+                }
+            }
+            LMPC_SYNC();
+            double rdy = 0.0;
+            if (lane < nd) {
+                double a = S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
+                for (int i = 0; i < nd; ++i) a = fma(Hg[(int64_t)i * P.np + lane], S.y[i], a);
+                rdy = a;
+                res = fmax(res, fabs(a));
+            }
+            const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
+            res = wave_max(res);
+            if ((mu <= P.tol_mu * scale && res <= P.tol_res * scale) || it >= P.max_iter) break;
+            // weights and K = Hy + R' diag(wh) R
+            double w1[2], wg[2], dl[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                w1[k] = W.z1[k] / W.s1[k];
+                wg[k] = W.zg[k] / W.sg[k];
+                dl[k] = 1.0 + w1[k] + wg[k];
+                if (r < P.rmax) S.wh[r] = r >= nr ? 0.0 : (r < p ? wg[k] : wg[k] * (1.0 + w1[k]) / dl[k]);
+            }
+#pragma unroll
+            for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+            {
+                const int g = lane >> 4, cc = lane & 15;
+#pragma unroll
+                for (int I = 0; I < 4; ++I)
+#pragma unroll
+                    for (int J = 0; J <= I; ++J)
+                        if (I < P.nt) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                acc[tid(I, J)][i] = Hg[(int64_t)(16 * I + 4 * i + g) * P.np + 16 * J + cc];
+                        }
+            }
+            LMPC_SYNC();
+            sym_tiles(P, S.R, ls, nr, S.wh, acc, lane);
+            {
+                const int g = lane >> 4, cc = lane & 15;
+#pragma unroll
+                for (int I = 0; I < 4; ++I)
+#pragma unroll
+                    for (int J = 0; J <= I; ++J)
+                        if (I < P.nt) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                S.KL[(16 * I + 4 * i + g) * ls + 16 * J + cc] = acc[tid(I, J)][i];
+                        }
+            }
+            LMPC_SYNC();
+            chol_floor(S, ls, nd, lane);
+            // Newton system for a complementarity target rc (per row): returns dy (lane j) and per-row
+            // directions; dz = W C dx + (z r_p - rc)/s, (H + C'WC) dx = -r_d - C'(z r_p - rc)/s
+            double ds1[2], dsg[2], dz1[2], dzg[2], dv[2];
+            auto newton = [&](const double rc1[2], const double rcg[2]) {
+                double rv[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int r = lane + 64 * k;
+                    rv[k] = 0.0;
+                    if (r < nr) {
+                        const double eg = (W.zg[k] * rpg[k] - rcg[k]) / W.sg[k];
+                        if (r < p) {
+                            S.q[r] = -eg;
+                        } else {
+                            const double e1 = (W.z1[k] * rp1[k] - rc1[k]) / W.s1[k];
+                            rv[k] = -rdv[k] + e1 + eg;
+                            S.q[r] = -eg + wg[k] * rv[k] / dl[k];
+                        }
+                    }
+                }
+                LMPC_SYNC();
+                const double rhs = lane < nd ? -rdy + rt_dot(S, ls, nr, S.q, lane) : 0.0;
+                chol_solve(S, ls, nd, rhs, S.dy, lane);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int r = lane + 64 * k;
+                    ds1[k] = dsg[k] = dz1[k] = dzg[k] = dv[k] = 0.0;
+                    if (r < nr) {
+                        const double td = row_dot(S, ls, nd, r, S.dy);
+                        double cg = td;
+                        if (r >= p) {
+                            dv[k] = (rv[k] + wg[k] * td) / dl[k];
+                            cg = td - dv[k];
+                            ds1[k] = -rp1[k] + dv[k];
+                            dz1[k] = (-rc1[k] - W.z1[k] * ds1[k]) / W.s1[k];
+                        }
+                        dsg[k] = -rpg[k] - cg;
+                        dzg[k] = (-rcg[k] - W.zg[k] * dsg[k]) / W.sg[k];
+                    }
+                }
+            };
+            auto max_step = [&]() {
+                double a = 1.0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int r = lane + 64 * k;
+                    if (r < nr) {
+                        if (dsg[k] < 0.0) a = fmin(a, -W.sg[k] / dsg[k]);
+                        if (dzg[k] < 0.0) a = fmin(a, -W.zg[k] / dzg[k]);
+                        if (r >= p) {
+                            if (ds1[k] < 0.0) a = fmin(a, -W.s1[k] / ds1[k]);
+                            if (dz1[k] < 0.0) a = fmin(a, -W.z1[k] / dz1[k]);
+                        }
+                    }
+                }
+                return wave_min(a);
+            };
+            double rc1[2], rcg[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                rc1[k] = W.s1[k] * W.z1[k];
+                rcg[k] = W.sg[k] * W.zg[k];
+            }
+            newton(rc1, rcg);
+            const double a_aff = max_step();
+            double ca = 0.0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                if (r < nr) {
+                    ca += (W.sg[k] + a_aff * dsg[k]) * (W.zg[k] + a_aff * dzg[k]);
+                    if (r >= p) ca += (W.s1[k] + a_aff * ds1[k]) * (W.z1[k] + a_aff * dz1[k]);
+                }
+            }
+            const double mu_aff = mc > 0.0 ? wave_sum(ca) / mc : 0.0;
+            const double sig = mu > 0.0 ? (mu_aff / mu) * (mu_aff / mu) * (mu_aff / mu) * mu : 0.0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                rc1[k] = W.s1[k] * W.z1[k] + ds1[k] * dz1[k] - sig;
+                rcg[k] = W.sg[k] * W.zg[k] + dsg[k] * dzg[k] - sig;
+            }
+            newton(rc1, rcg);
+            const double a = fmin(1.0, HQ_FRAC * max_step());
+            if (lane < nd) S.y[lane] += a * S.dy[lane];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                W.v[k] += a * dv[k];
+                W.s1[k] += a * ds1[k];
+                W.z1[k] += a * dz1[k];
+                W.sg[k] += a * dsg[k];
+                W.zg[k] += a * dzg[k];
+            }
+            LMPC_SYNC();
+        }
+        if (it >= P.max_iter) st = 1;
+        if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it;
+        // ---- outputs: w_l = max(0, D_l Z y - g) for the final y, x += Z y ------------------------------
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = lane + 64 * k;
+            if (r >= p && r < nr) wo[r] = fmax(0.0, row_dot(S, ls, nd, r, S.y) - W.bd[k]);
+        }
+        double xn = 0.0;
+        if (lane < P.n) {
+            const gdouble* zr = Z + (int64_t)lane * P.np;
+            double a = S.x[lane];
+            for (int j = 0; j < nd; ++j) a = fma(zr[j], S.y[j], a);
+            xn = a;
+            xout[((int64_t)b * P.L + l) * P.n + lane] = a;
+        }
+        LMPC_SYNC();
+        if (lane < P.n) S.x[lane] = xn;
+        LMPC_GSYNC();
+        if (m > 0) {
+            zc ^= 1;
+            nd = nd_next;
+        }
+        p = nr;
+    }
+    // non-finite result: zeros, LMPC_QP_NAN
+    bool bad = false;
+    for (int l = 0; l < P.L; ++l)
+        if (lane < P.n && !isfinite(xout[((int64_t)b * P.L + l) * P.n + lane])) bad = true;
+    for (int r = lane; r < P.slack_len; r += 64)
+        if (!isfinite(wout[(int64_t)b * P.slack_len + r])) bad = true;
+    if (__ballot(bad)) {
+        for (int l = 0; l < P.L; ++l)
+            if (lane < P.n) xout[((int64_t)b * P.L + l) * P.n + lane] = 0.0;
+        for (int r = lane; r < P.slack_len; r += 64) wout[(int64_t)b * P.slack_len + r] = 0.0;
+        st = 2;
+    }
+    if (status && lane == 0) status[b] = st;
+}
+
+hipError_t launch_hoqp(const HoqpDev& P, const double* rec, int batch, double* x, double* w, int32_t* status,
+                       int32_t* iters, double* scratch, hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    const size_t lds = hq_lds_doubles(P) * sizeof(double);
+    hipLaunchKernelGGL(lmpc_hoqp_kernel, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters, scratch,
+                       batch);
+    return hipGetLastError();
+}
+
+}  // namespace lmpc

@@ -183,7 +183,11 @@ def qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
     n, m = H.shape[0], D.shape[0]
     x = np.array(x0, dtype=np.longdouble)
     scale = 1.0 + np.max(np.abs(f)) if m else 1.0
-    W = [i for i in range(m) if abs(float(D[i] @ x) - f[i]) <= tol * scale]
+    # rows that are zero up to rounding (a higher level's row projected on a null space it is orthogonal to)
+    # constrain nothing: they never enter the working set
+    dscale = float(np.max(np.abs(D))) if m else 0.0
+    live = [i for i in range(m) if float(np.max(np.abs(D[i]))) > 1e-12 * dscale]
+    W = [i for i in live if abs(float(D[i] @ x) - f[i]) <= tol * scale]
     # keep a linearly independent working set
     Wi = []
     for i in W:
@@ -213,11 +217,14 @@ def qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
             W.pop(int(np.argmin(lam)))
             continue
         alpha, block = 1.0, -1
-        for i in range(m):
+        pn = float(np.max(np.abs(p)))
+        for i in live:
             if i in W:
                 continue
             dp = float(D[i] @ p)
-            if dp > 1e-300:
+            # a row moving at rounding level along p is not blocking: it lies in the span of the working set
+            # (e.g. a zero inequality row's slack bound 0 - w <= 0 duplicates -w <= 0)
+            if dp > 1e-13 * pn * float(np.max(np.abs(D[i]))):
                 a = float((f[i] - D[i] @ x)) / dp
                 if a < alpha:
                     alpha, block = a, i

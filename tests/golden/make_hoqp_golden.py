@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Generate the hierarchical-QP fixtures (tests/golden/hoqp_golden.npz).  Run in the
+build container; the fixture is committed and the GPU box only reads it.
+
+Groups (each one batch of same-shaped hierarchies, packed as include/lmpc/lmpc_hoqp.h records):
+  wbc   -- 16 WBC-shaped hierarchies (legged_mpc_control_amd/wbc.py: wbc.cpp:93-96 on synthetic Go1-scale
+           dynamics; 42 variables, levels (30 eq, 44 ineq), (18 eq), (12 eq)); every variable is pinned by
+           the last level, so its x is comparable across solvers;
+  rand3 -- random three-level hierarchies over 8 variables with inequalities on levels 0-2 (the draws the
+           reference's slack pairing leaves feasible, HoQp.cpp:58 vs :176-182);
+  ref   -- the reference's own test data (src/test/ho_qp_test.cpp:10-22, regenerated bit for bit).
+Expected values come from oracle/hoqp.py (exact primal active set in x87 extended precision, Eigen's
+FullPivLU kernel basis); every level is certified by its KKT conditions here, and the wbc group's levels
+are cross-checked against scipy's SLSQP on the same level QPs.  No reference-produced outputs exist (qpOASES,
+Eigen and OCS2 are absent; the reference test prints its results without asserting values)."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from legged_mpc_control_amd import hoqp as HQ  # noqa: E402
+from legged_mpc_control_amd import wbc as W  # noqa: E402
+from oracle import hoqp as Q  # noqa: E402
+
+OUT = os.path.join(HERE, "hoqp_golden.npz")
+
+
+def oracle_chain(tasks):
+    lv = []
+    for t in tasks:
+        lv.append(Q.HoQp(Q.Task(t.a, t.b, t.d, t.f), lv[-1] if lv else None))
+    for k, h in enumerate(lv):
+        kkt = h.kkt()
+        assert kkt <= 1e-8 * (1.0 + float(np.max(np.abs(h.c)))), (k, kkt)
+    return lv
+
+
+def slsqp_check(h):
+    """Independent solve of one level QP (the oracle's H, c, D, f) with scipy SLSQP from the oracle's start."""
+    from scipy.optimize import minimize
+
+    H, c, D, f = h.H, h.c, h.D, h.f
+    fun = lambda z: 0.5 * z @ H @ z + c @ z
+    jac = lambda z: H @ z + c
+    cons = [{"type": "ineq", "fun": lambda z: f - D @ z, "jac": lambda z: -D}] if D.shape[0] else []
+    r = minimize(fun, np.zeros(H.shape[0]), jac=jac, constraints=cons, method="SLSQP",
+                 options=dict(ftol=1e-14, maxiter=500))
+    return abs(r.fun - fun(h.qp_solution)) / (1.0 + abs(fun(h.qp_solution)))
+
+
+def random_task(rng, n, ne, ni, tight):
+    a = rng.standard_normal((ne, n))
+    d = rng.standard_normal((ni, n))
+    f = rng.uniform(-0.5, 0.2, ni) if tight else rng.uniform(0.5, 2.0, ni)
+    return HQ.Task(a, rng.standard_normal(ne), d, f)
+
+
+def group(chains, pinned):
+    dims = HQ.dims_of(chains[0])
+    rec = np.stack([HQ.pack(c, dims) for c in chains])
+    L, n = dims.num_levels, dims.num_vars
+    S = sum(dims.ineq_rows[:L])
+    xs = np.zeros((len(chains), L, n))
+    ws = np.zeros((len(chains), S))
+    for b, c in enumerate(chains):
+        lv = oracle_chain(c)
+        for k, h in enumerate(lv):
+            xs[b, k] = h.solution()
+        ws[b] = lv[-1].stacked_slack
+    d = np.array([n, L] + list(dims.eq_rows) + list(dims.ineq_rows), dtype=np.int32)
+    return dict(dims=d, rec=rec, x=xs, w=ws, pinned=np.array(pinned))
+
+
+def main():
+    out = {}
+    wbc = [W.synth_wbc_tasks(s) for s in range(16)]
+    g = group(wbc, True)
+    worst = 0.0
+    for c in wbc[:4]:
+        for h in oracle_chain(c):
+            worst = max(worst, slsqp_check(h))
+    print(f"wbc: SLSQP objective agreement {worst:.1e}")
+    assert worst < 1e-6
+    out.update({f"wbc_{k}": v for k, v in g.items()})
+    rand, infeasible = [], []
+    seed = 0
+    while len(rand) < 12:
+        rng = np.random.default_rng(1000 + seed)
+        c = [random_task(rng, 8, 2, 3, seed % 2 == 0), random_task(rng, 8, 2, 2, False),
+             random_task(rng, 8, 3, 2, seed % 3 == 0)]
+        try:
+            oracle_chain(c)
+            rand.append(c)
+        except ValueError:
+            infeasible.append(seed)
+        seed += 1
+    out.update({f"rand3_{k}": v for k, v in group(rand, False).items()})
+    out["rand3_infeasible_seeds"] = np.array(infeasible, dtype=np.int32)
+    t0, t1 = Q.reference_test_tasks()
+    ref = [HQ.Task(t0.a, t0.b, t0.d, t0.f), HQ.Task(t1.a, t1.b, t1.d, t1.f)]
+    out.update({f"ref_{k}": v for k, v in group([ref], False).items()})
+    np.savez_compressed(OUT, **out)
+    print(f"wrote {OUT}: wbc {len(wbc)}, rand3 {len(rand)} (quirk-infeasible seeds {infeasible[:5]}...), ref 1")
+
+
+if __name__ == "__main__":
+    main()

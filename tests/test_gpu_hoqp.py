@@ -1,0 +1,179 @@
+"""GPU parity of the batched hierarchical QP (lmpc_hoqp.hip through include/lmpc/lmpc_hoqp.h; SURVEY.md 8f
+row 4) against the committed fixtures of the CPU restatement (tests/golden/hoqp_golden.npz, oracle/hoqp.py).
+
+Compared (include/lmpc/lmpc_hoqp.h, "Numerics"): every level's equality values A_l x_l, every slack, and the
+last level's x where the hierarchy pins every variable (the WBC).  Tolerance 1e-6 relative to the data's
+scale (the reference test's own precision, ho_qp_test.cpp:31)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-6
+
+
+def load(group):
+    d = np.load(os.path.join(GOLDEN, "hoqp_golden.npz"), allow_pickle=False)
+    return {k[len(group) + 1:]: d[k] for k in d.files if k.startswith(group + "_")}
+
+
+def dims_from(arr):
+    from legged_mpc_control_amd import _native as N
+
+    d = N.LmpcHoqpDims()
+    d.num_vars, d.num_levels = int(arr[0]), int(arr[1])
+    for l in range(N.HOQP_MAX_LEVELS):
+        d.eq_rows[l] = int(arr[2 + l])
+        d.ineq_rows[l] = int(arr[6 + l])
+    return d
+
+
+def unpack(rec, dims):
+    """record -> per level (a, b, d, f)"""
+    n, out, o = dims.num_vars, [], 0
+    for l in range(dims.num_levels):
+        m, s = dims.eq_rows[l], dims.ineq_rows[l]
+        a = rec[o:o + m * n].reshape(m, n); o += m * n
+        b = rec[o:o + m]; o += m
+        d = rec[o:o + s * n].reshape(s, n); o += s * n
+        f = rec[o:o + s]; o += s
+        out.append((a, b, d, f))
+    return out
+
+
+def check_against(rec, dims, x, w, x_ref, w_ref, pinned):
+    levels = unpack(rec, dims)
+    scale = 1.0 + max(float(np.max(np.abs(rec))), float(np.max(np.abs(x_ref))))
+    for l, (a, b, d, f) in enumerate(levels):
+        if a.shape[0]:
+            err = np.max(np.abs(a @ x[l] - a @ x_ref[l]))
+            assert err <= TOL * scale, f"level {l}: A x differs by {err:.2e}"
+    if w_ref.size:
+        err = np.max(np.abs(w - w_ref))
+        assert err <= TOL * scale, f"slacks differ by {err:.2e}"
+    if pinned:
+        err = np.max(np.abs(x[-1] - x_ref[-1])) / (1.0 + np.max(np.abs(x_ref[-1])))
+        assert err <= TOL, f"final x differs by {err:.2e}"
+    # every level's inequalities hold within its slacks, on its own solution
+    o = 0
+    for l, (a, b, d, f) in enumerate(levels):
+        s = d.shape[0]
+        if s:
+            assert np.all(d @ x[l] <= f + w[o:o + s] + TOL * scale)
+        o += s
+    assert np.all(w >= 0.0)
+
+
+@pytest.fixture(scope="module")
+def hq():
+    import torch
+
+    # torch's HIP runtime first: initialised after another HIP client in the process it finds no device
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    torch.cuda.init()
+    from legged_mpc_control_amd import hoqp
+
+    return hoqp
+
+
+@pytest.mark.parametrize("group", ["wbc", "rand3", "ref"])
+def test_golden_groups(hq, group):
+    g = load(group)
+    dims = dims_from(g["dims"])
+    B = g["rec"].shape[0]
+    solver = hq.HoqpBatch(dims, B)
+    x, w, st, it = solver.solve(g["rec"])
+    assert np.all(st == 0), st
+    assert np.all((it > 0) & (it < 60))
+    for b in range(B):
+        check_against(g["rec"][b], dims, x[b], w[b], g["x"][b], g["w"][b], bool(g["pinned"]))
+
+
+def test_reference_two_task_checks(hq):
+    """ho_qp_test.cpp:20-46 through the Python mirror of HoQp.h, on the reference's own data."""
+    g = load("ref")
+    dims = dims_from(g["dims"])
+    (a0, b0, d0, f0), (a1, b1, d1, f1) = unpack(g["rec"][0], dims)
+    t0, t1 = hq.Task(a0, b0, d0, f0), hq.Task(a1, b1, d1, f1)
+    h0 = hq.HoQp(t0)
+    h1 = hq.HoQp(t1, h0)
+    x0, x1 = h0.getSolutions(), h1.getSolutions()
+    s0, s1 = h0.getStackedSlackSolutions(), h1.getStackedSlackSolutions()
+    assert s0.shape == (2,) and s1.shape == (4,)
+    assert h0.status == 0 and h1.status == 0
+    prec = 1e-6
+    approx = lambda u, v: np.linalg.norm(u - v) <= prec * min(np.linalg.norm(u), np.linalg.norm(v))
+    if np.allclose(s0, 0.0):
+        assert approx(a0 @ x0, b0)
+    if np.allclose(s1, 0.0):
+        assert approx(a1 @ x1, b1) and approx(a0 @ x1, b0)
+    assert np.all(d0 @ x0 <= f0 + s0 + 1e-9)
+    assert np.all(d1 @ x1 <= f1 + s1[:2] + 1e-9)  # the test indexes the stacked slacks from the front
+    assert h1.getSlackedNumVars() == 4 and h1.getStackedTasks().d.shape == (4, 4)
+    check_against(g["rec"][0], dims, np.stack([x0, x1]), s1, g["x"][0], g["w"][0], False)
+
+
+def test_device_path_and_batch_position_invariance(hq):
+    """The device entry point on torch buffers equals the host path bitwise; an instance's result does not
+    depend on its position in the batch."""
+    import torch
+
+    g = load("wbc")
+    dims = dims_from(g["dims"])
+    rec = np.concatenate([g["rec"], g["rec"][::-1]])
+    B = rec.shape[0]
+    solver = hq.HoqpBatch(dims, B)
+    x, w, st, _ = solver.solve(rec)
+    assert np.array_equal(x[:16], x[16:][::-1]) and np.array_equal(w[:16], w[16:][::-1])
+    d_rec = torch.from_numpy(rec).cuda()
+    d_x = torch.zeros((B, dims.num_levels, dims.num_vars), dtype=torch.float64, device="cuda")
+    d_w = torch.zeros((B, solver.slack_len), dtype=torch.float64, device="cuda")
+    d_st = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    solver.solve_device(d_rec, d_x, d_w, d_st)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_x.cpu().numpy(), x) and np.array_equal(d_w.cpu().numpy(), w)
+    assert np.array_equal(d_st.cpu().numpy(), st)
+
+
+def test_wbc_batch_properties_at_scale(hq):
+    """4096 WBC hierarchies (the bench's batch): all converge; the highest-priority equalities (floating-base
+    EoM, contact constraints) hold exactly on the final solution; torque limits and friction pyramids hold
+    within their slacks; the slacks are nonnegative."""
+    from legged_mpc_control_amd import wbc as W
+
+    B = 4096
+    chains = [W.synth_wbc_tasks(10_000 + i) for i in range(64)]
+    dims = hq.dims_of(chains[0])
+    base = np.stack([hq.pack(c, dims) for c in chains])
+    rec = np.tile(base, (B // 64, 1))
+    solver = hq.HoqpBatch(dims, B)
+    x, w, st, it = solver.solve(rec)
+    assert np.all(st == 0)
+    assert np.array_equal(x[:64], x[64:128])
+    for b in range(64):
+        (a0, b0, d0, f0) = unpack(rec[b], dims)[0]
+        xf = x[b, -1]
+        assert np.max(np.abs(a0 @ xf - b0)) <= 1e-7 * (1 + np.max(np.abs(b0)))
+        assert np.all(d0 @ xf <= f0 + w[b] + 1e-7)
+    assert np.all(w >= 0.0)
+
+
+def test_level_without_equalities(hq):
+    """A level with only inequality rows (the reference hands qpOASES a zero Hessian block there; here the
+    1e-12 term): runs, converges, keeps the higher level's equality values and meets its own rows."""
+    rng = np.random.default_rng(5)
+    n = 6
+    t0 = hq.Task(rng.standard_normal((3, n)), rng.standard_normal(3), rng.standard_normal((2, n)),
+                 rng.uniform(0.5, 1.0, 2))
+    t1 = hq.Task(None, None, rng.standard_normal((3, n)), rng.uniform(-0.2, 0.5, 3))
+    t2 = hq.Task(rng.standard_normal((4, n)), rng.standard_normal(4), None, None)
+    chain = [t0, t1, t2]
+    dims = hq.dims_of(chain)
+    x, w, st, _ = hq.HoqpBatch(dims, 1).solve(hq.pack(chain, dims)[None])
+    assert st[0] == 0
+    assert np.allclose(t0.a @ x[0, 2], t0.a @ x[0, 0], atol=1e-8)
+    assert np.all(t1.d @ x[0, 1] <= t1.f + w[0, 2:5] + 1e-8)

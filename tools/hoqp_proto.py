@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Dev tool (CPU): numpy replica of the planned HoQp device algorithm, to size iterations and accuracy before
+writing the kernel.  Per level (HoQp.cpp:65-174): G = A Z, Hy = G'G + 1e-12 I, c = G'(A x - b), frozen rows
+P = D_prev Z with the reference's slack pairing, current rows Dz = D Z; the level QP over (y, v) solved by a
+Mehrotra interior point with the slacks v eliminated (K = Hy + R' diag(w) R, R = [P; Dz]); x += Z y;
+Z <- Z ker(G) (Eigen FullPivLU basis).  Compared against oracle/hoqp.py (exact active set, x87)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import hoqp as Q  # noqa: E402
+
+
+PIV_FLOOR = 1e-13   # relative to the largest diagonal entry of K
+PIV_BIG = 1e64      # a pivot below the floor is replaced by this: that Cholesky coordinate does not move
+
+
+def chol_floor(K):
+    """Cholesky with a pivot floor: K = A'A + 1e-12 I is singular in double along ker(A) wherever no
+    inequality weight acts (1e-12 is below the rounding of A'A), so pivots at rounding level freeze their
+    coordinate instead of failing; along those directions the level's objective is flat at double precision."""
+    n = K.shape[0]
+    L = np.zeros_like(K)
+    A = K.copy()
+    thr = PIV_FLOOR * max(1.0, float(np.max(np.diag(K)))) if n else 0.0
+    for k in range(n):
+        p = A[k, k]
+        if not p > thr:
+            p = PIV_BIG
+        d = np.sqrt(p)
+        L[k, k] = d
+        L[k + 1:, k] = A[k + 1:, k] / d
+        A[k + 1:, k + 1:] -= np.outer(L[k + 1:, k], L[k + 1:, k])
+    return L
+
+
+def chol_solve(L, r):
+    n = L.shape[0]
+    u = np.zeros(n)
+    for i in range(n):
+        u[i] = (r[i] - L[i, :i] @ u[:i]) / L[i, i]
+    x = np.zeros(n)
+    for i in range(n - 1, -1, -1):
+        x[i] = (u[i] - L[i + 1:, i] @ x[i + 1:]) / L[i, i]
+    return x
+
+
+def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1e-13)), frac=0.99, stats=None):
+    """min 1/2 y'Hy y + c'y + 1/2 v'v  s.t. -v <= 0, P y <= h, Dz y - v <= g.  Returns (y, v, iters)."""
+    nd, p, s = Hy.shape[0], P.shape[0], Dz.shape[0]
+    m = 2 * s + p
+    y = np.zeros(nd)
+    v = np.maximum(0.0, -g) + 1.0 if s else np.zeros(0)
+    # slacks of the three blocks; start them (and the duals) at least at 1
+    s1 = np.maximum(v, 1.0)
+    s2 = np.maximum(h - P @ y, 1.0) if p else np.zeros(0)
+    s3 = np.maximum(g - Dz @ y + v, 1.0) if s else np.zeros(0)
+    z1, z2, z3 = np.ones(s), np.ones(p), np.ones(s)
+    scale = 1.0 + max(np.max(np.abs(c)) if nd else 0.0, np.max(np.abs(h)) if p else 0.0,
+                      np.max(np.abs(g)) if s else 0.0)
+    it = 0
+    for it in range(max_iter):
+        # residuals: r_d = H x + c + C'z, r_p = C x + sigma - d
+        rdy = Hy @ y + c + (P.T @ z2 if p else 0) + (Dz.T @ z3 if s else 0)
+        rdv = v - z1 - z3
+        rp1 = -v + s1
+        rp2 = P @ y + s2 - h
+        rp3 = Dz @ y - v + s3 - g
+        sig = np.concatenate([s1, s2, s3])
+        zz = np.concatenate([z1, z2, z3])
+        mu = sig @ zz / m if m else 0.0
+        res = max(np.max(np.abs(rdy)) if nd else 0.0, np.max(np.abs(rdv)) if s else 0.0,
+                  np.max(np.abs(np.concatenate([rp1, rp2, rp3]))) if m else 0.0)
+        if mu <= tol * scale and res <= float(os.environ.get('RTOL', 1e-10)) * scale:
+            break
+        w1, w2, w3 = z1 / s1, z2 / s2, z3 / s3
+        dlt = 1.0 + w1 + w3
+        w3h = w3 * (1.0 + w1) / dlt
+        K = Hy + (P.T @ (w2[:, None] * P) if p else 0) + (Dz.T @ (w3h[:, None] * Dz) if s else 0)
+        L = chol_floor(K)
+
+        def newton(rc1, rc2, rc3):
+            # dz = W (C dx) + (z r_p - r_c)/sigma ; (H + C'WC) dx = -r_d - C'(z r_p - r_c)/sigma
+            e1 = (z1 * rp1 - rc1) / s1
+            e2 = (z2 * rp2 - rc2) / s2
+            e3 = (z3 * rp3 - rc3) / s3
+            ry = -rdy - (P.T @ e2 if p else 0) - (Dz.T @ e3 if s else 0)
+            rv = -rdv + e1 + e3
+            rhs = ry + (Dz.T @ (w3 * rv / dlt) if s else 0)
+            dy = chol_solve(L, rhs)
+            dv = (rv + w3 * (Dz @ dy if s else 0)) / dlt if s else np.zeros(0)
+            # C dx per block
+            c1, c2, c3 = -dv, (P @ dy if p else np.zeros(0)), (Dz @ dy - dv if s else np.zeros(0))
+            ds1, ds2, ds3 = -rp1 - c1, -rp2 - c2, -rp3 - c3
+            dz1 = (-rc1 - z1 * ds1) / s1
+            dz2 = (-rc2 - z2 * ds2) / s2
+            dz3 = (-rc3 - z3 * ds3) / s3
+            return dy, dv, (ds1, ds2, ds3), (dz1, dz2, dz3)
+
+        def max_step(vals, dirs):
+            a = 1.0
+            for x, d in zip(vals, dirs):
+                neg = d < 0
+                if np.any(neg):
+                    a = min(a, float(np.min(-x[neg] / d[neg])))
+            return a
+
+        dy, dv, ds, dz = newton(s1 * z1, s2 * z2, s3 * z3)
+        a_aff = max_step((s1, s2, s3, z1, z2, z3), ds + dz)
+        mu_aff = sum(((sx + a_aff * d1) @ (zx + a_aff * d2)) for sx, d1, zx, d2 in
+                     zip((s1, s2, s3), ds, (z1, z2, z3), dz)) / m
+        sc = (mu_aff / mu) ** 3 * mu
+        dy, dv, ds2_, dz2_ = newton(s1 * z1 + ds[0] * dz[0] - sc, s2 * z2 + ds[1] * dz[1] - sc,
+                                    s3 * z3 + ds[2] * dz[2] - sc)
+        a = min(1.0, frac * max_step((s1, s2, s3, z1, z2, z3), ds2_ + dz2_))
+        y = y + a * dy
+        v = v + a * dv
+        s1, s2, s3 = s1 + a * ds2_[0], s2 + a * ds2_[1], s3 + a * ds2_[2]
+        z1, z2, z3 = z1 + a * dz2_[0], z2 + a * dz2_[1], z3 + a * dz2_[2]
+    if stats is not None:
+        stats.append(it)
+    if s and os.environ.get("VEXACT"):
+        v = np.maximum(0.0, Dz @ y - g)
+    if os.environ.get("VERBOSE"):
+        print(f"    ipm it {it} mu {mu:.1e} res {res:.1e} scale {scale:.1e}")
+    return y, v, it
+
+
+def hoqp_device(tasks, stats=None):
+    """tasks: list of oracle Task.  Returns per-level x and w, as the chain of HoQp objects would."""
+    n = max(tasks[0].a.shape[1], tasks[0].d.shape[1])
+    Z = np.eye(n)
+    x = np.zeros(n)
+    stk_d = np.zeros((0, n))  # stacked rows, current level first (HoQp.cpp:60)
+    stk_f = np.zeros(0)
+    stk_w = np.zeros(0)       # stacked slacks, current level last (HoQp.cpp:176-182)
+    xs, ws = [], []
+    for t in tasks:
+        nd = Z.shape[1]
+        has_eq = t.a.shape[0] > 0
+        d = t.d if t.d.shape[1] else np.zeros((0, n))
+        if has_eq:
+            G = t.a @ Z
+            Hy = G.T @ G + 1e-12 * np.eye(nd)
+            c = G.T @ (t.a @ x - t.b)
+        else:
+            Hy = 1e-12 * np.eye(nd)
+            c = np.zeros(nd)
+        P = stk_d @ Z
+        h = stk_f - stk_d @ x + stk_w
+        Dz = d @ Z
+        g = t.f - d @ x if d.shape[0] else np.zeros(0)
+        y, v, _ = level_ipm(Hy, c, P, h, Dz, g, stats=stats)
+        x = x + Z @ y
+        xs.append(x.copy())
+        ws.append(v.copy())
+        stk_d = np.vstack([d, stk_d])
+        stk_f = np.concatenate([t.f if d.shape[0] else np.zeros(0), stk_f])
+        stk_w = np.concatenate([stk_w, v])
+        if has_eq:
+            Z = Z @ Q.fullpivlu_kernel(t.a @ Z)
+    return xs, ws
+
+
+def random_task(rng, n, ne, ni, tight):
+    a = rng.standard_normal((ne, n))
+    d = rng.standard_normal((ni, n))
+    f = rng.uniform(-0.5, 0.2, ni) if tight else rng.uniform(0.5, 2.0, ni)
+    return Q.Task(a, rng.standard_normal(ne), d, f)
+
+
+def compare(tasks, label, stats):
+    t0 = time.time()
+    lv = []
+    for t in tasks:
+        lv.append(Q.HoQp(t, lv[-1] if lv else None))
+    t1 = time.time()
+    xs, ws = hoqp_device(tasks, stats)
+    ex = max(float(np.max(np.abs(xd - h.solution()))) / (1 + float(np.max(np.abs(h.solution()))))
+             for xd, h in zip(xs, lv))
+    ew = max(float(np.max(np.abs(wd - h.w_sol))) if wd.size else 0.0 for wd, h in zip(ws, lv))
+    eax = max(float(np.max(np.abs(t.a @ (xd - h.solution())))) if t.a.shape[0] else 0.0
+              for t, xd, h in zip(tasks, xs, lv))
+    xf = float(np.max(np.abs(xs[-1] - lv[-1].solution()))) / (1 + float(np.max(np.abs(lv[-1].solution()))))
+    if os.environ.get("VERBOSE"):
+        for k, (t, xd, wd, h) in enumerate(zip(tasks, xs, ws, lv)):
+            print(f"  level {k}: |A dx| {np.max(np.abs(t.a @ (xd - h.solution()))) if t.a.shape[0] else 0:.1e} "
+                  f"|dw| {np.max(np.abs(wd - h.w_sol)) if wd.size else 0:.1e} |dx| {np.max(np.abs(xd - h.solution())):.1e}"
+                  f" w>0: {int(np.sum(h.w_sol > 1e-9))}")
+    return ex, ew, eax, xf, t1 - t0
+
+
+def main():
+    stats = []
+    t0, t1 = Q.reference_test_tasks()
+    print("reference test:", compare([t0, t1], "ref", stats))
+    worst = np.zeros(4)
+    for seed in range(12):
+        rng = np.random.default_rng(100 + seed)
+        n = 8
+        tasks = [random_task(rng, n, 2, 3, tight=seed % 2 == 0), random_task(rng, n, 2, 2, tight=False),
+                 random_task(rng, n, 3, 2, tight=seed % 3 == 0)]
+        try:
+            r = compare(tasks, "rand", stats)
+        except ValueError:
+            continue
+        worst = np.maximum(worst, r[:4])
+    print("random 3-level: max rel x err (per level, final) / w / A dx:", worst)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from legged_mpc_control_amd import wbc as W  # noqa: E402
+    worst = np.zeros(4)
+    tt = 0.0
+    for seed in range(int(sys.argv[1]) if len(sys.argv) > 1 else 20):
+        tasks = W.synth_wbc_tasks(seed)
+        r = compare(tasks, "wbc", stats)
+        worst = np.maximum(worst, r[:4])
+        tt += r[4]
+    print("wbc-shaped: max rel x err (levels, final) / w / A dx:", worst, f"oracle {tt:.1f}s")
+    print("IPM iterations per level: mean %.1f max %d" % (np.mean(stats), np.max(stats)))
+
+
+if __name__ == "__main__":
+    main()
