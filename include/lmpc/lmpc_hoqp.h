@@ -54,7 +54,7 @@ typedef struct {
 typedef struct {
     int32_t max_iter;   /* interior-point iterations per level (default 60) */
     double tol_mu;      /* stop: mean complementarity <= tol_mu * scale (default 1e-13) */
-    double tol_res;     /* stop: max primal / dual residual <= tol_res * scale (default 1e-10) */
+    double tol_res;     /* stop: max primal / dual residual <= tol_res * scale (default 1e-7) */
 } lmpc_hoqp_options;
 
 typedef struct lmpc_hoqp_ctx lmpc_hoqp_ctx;

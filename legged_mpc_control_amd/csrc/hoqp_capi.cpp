@@ -147,7 +147,7 @@ void lmpc_hoqp_options_default(lmpc_hoqp_options* o) {
     if (!o) return;
     o->max_iter = 60;
     o->tol_mu = 1e-13;
-    o->tol_res = 1e-10;
+    o->tol_res = 1e-7;
 }
 
 int64_t lmpc_hoqp_record_len(const lmpc_hoqp_dims* d) {

@@ -39,6 +39,33 @@ constexpr double HQ_FRAC = 0.99;        // fraction of the step to the boundary
 
 typedef __attribute__((address_space(3))) int lint;
 
+}  // namespace
+
+// Diagnostic build only (-DLMPC_STAMPS): per-phase cycle counters of instance 0..4095 (tools/hoqp_stamps.py):
+// 0 setup (G, c, Hy), 1 FullPivLU + basis, 2 constraint rows + bounds, 3 residuals, 4 K on the matrix cores,
+// 5 Cholesky, 6 Newton systems + steps, 7 outputs.
+#ifdef LMPC_STAMPS
+__device__ unsigned long long lmpc_hoqp_stamps[4096][8];
+#define HSTAMP_DECL unsigned long long _hs_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long _hs_t0 = __builtin_readcyclecounter();
+#define HSTAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _hs_acc[i] += _t - _hs_t0; _hs_t0 = _t; } while (0)
+#define HSTAMP_FLUSH(b) do { if (threadIdx.x == 0 && (b) < 4096) for (int _i = 0; _i < 8; ++_i) { lmpc_hoqp_stamps[b][_i] = _hs_acc[_i]; lmpc_hoqp_substamps[b][_i] = _hq_acc[_i]; } } while (0)
+// sub-phases of one interior-point iteration: 0 q, 1 R'q, 2 substitutions, 3 R dy + directions, 4 step length,
+// 5 mu_aff + corrector targets, 6 update
+__device__ unsigned long long lmpc_hoqp_substamps[4096][8];
+#define HQSUB_DECL unsigned long long _hq_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long _hq_t0 = 0;
+#define HQSUB_START() do { _hq_t0 = __builtin_readcyclecounter(); } while (0)
+#define HQSUB(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _hq_acc[i] += _t - _hq_t0; _hq_t0 = _t; } while (0)
+#else
+#define HQSUB_DECL
+#define HQSUB_START() do {} while (0)
+#define HQSUB(i) do {} while (0)
+#define HSTAMP_DECL
+#define HSTAMP(i) do {} while (0)
+#define HSTAMP_FLUSH(b) do {} while (0)
+#endif
+
+namespace {
+
 struct HS {
     ldouble* R;    // rmax x ls: constraint rows in y (columns nd..np-1 zero)
     ldouble* KL;   // kmax x ls: G (setup, FullPivLU) then K and its Cholesky factor (lower)
@@ -166,73 +193,154 @@ __device__ __forceinline__ void sym_tiles(const HoqpDev& P, const ldouble* M, in
     }
 }
 
-// Cholesky factor of K (nd x nd, lower, in place, row-parallel: lane i = row i) with a pivot floor;
-// dI[k] = 1 / L_kk.
-__device__ void chol_floor(const HS& S, int ls, int nd, int lane) {
-    double dmax = lane < nd ? S.KL[lane * ls + lane] : 0.0;
-    dmax = wave_max(dmax);
+// Cholesky factor of K (nd x nd, lower) with a pivot floor, lane i = row i held in registers (kr[j] = K_ij,
+// statically indexed: NP = np unrolls every loop); column k is broadcast through LDS (S.dy as the buffer) and
+// applied to every row at once.  The factor goes back to S.KL (lower part), dI[k] = 1 / L_kk.
+template <int NP>
+__device__ __attribute__((noinline)) void chol_floor(const HS& S, int ls, int nd, int lane) {
+    double kr[NP];
+    const bool live = lane < nd;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) kr[j] = (live && j < nd) ? S.KL[lane * ls + j] : 0.0;
+    const double dmax = wave_max(live ? S.KL[lane * ls + lane] : 0.0);
     const double thr = HQ_PIV_FLOOR * fmax(1.0, dmax);
-    for (int k = 0; k < nd; ++k) {
-        const double pkk = S.KL[k * ls + k];
-        const double piv = pkk > thr ? pkk : HQ_PIV_BIG;
-        const double inv = 1.0 / sqrt(piv);
-        LMPC_SYNC();
-        double l = 0.0;
-        if (lane == k) {
-            S.KL[k * ls + k] = piv * inv;
-            S.dI[k] = inv;
-        } else if (lane > k && lane < nd) {
-            l = S.KL[lane * ls + k] * inv;
-            S.KL[lane * ls + k] = l;
+    ldouble* col = S.dy;
+    double di = 0.0;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        if (k < nd) {
+            const double pkk = readlane_f64(kr[k], k);
+            const double piv = pkk > thr ? pkk : HQ_PIV_BIG;
+            double inv = rsq_nr(piv);
+            inv = inv * fma(-0.5 * piv * inv, inv, 1.5);  // second Newton step: 1/sqrt to rounding
+            const double l = kr[k] * inv;  // L_ik on rows i > k
+            kr[k] = lane == k ? piv * inv : l;
+            di = lane == k ? inv : di;
+            if (lane < NP) col[lane] = lane > k ? l : 0.0;  // col = S.dy has np = NP entries
+            LMPC_SYNC();
+#pragma unroll
+            for (int j = k + 1; j < NP; ++j) kr[j] = fma(-l, col[j], kr[j]);  // rows <= k: upper part, unused
+            LMPC_SYNC();
         }
-        LMPC_SYNC();
-        if (lane > k && lane < nd)
-            for (int j = k + 1; j <= lane; ++j) S.KL[lane * ls + j] -= l * S.KL[j * ls + k];
-        LMPC_SYNC();
     }
+    // store the unit lower factor Lt = L diag(1/L_kk) (K = Lt D^2 Lt', D = diag(L_kk)): its substitutions need
+    // no division per step
+    if (live) S.dI[lane] = di;
+    LMPC_SYNC();
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        if (live && j < lane) S.KL[lane * ls + j] = kr[j] * S.dI[j];
+    LMPC_SYNC();
 }
 
-// K u = rhs with K = L L': rhs in lane i (i < nd); returns u in lane i, also stored to out[i].
-__device__ double chol_solve(const HS& S, int ls, int nd, double rhs, ldouble* out, int lane) {
-    const double di = lane < nd ? S.dI[lane] : 0.0;
-    double acc = lane < nd ? rhs : 0.0;
-    double u = 0.0;
-    for (int k = 0; k < nd; ++k) {  // L w = rhs
-        const double lik = (lane > k && lane < nd) ? S.KL[lane * ls + k] : 0.0;
-        const double wk = readlane_f64(acc * di, k);
-        if (lane == k) u = wk;
-        acc = fma(-lik, wk, acc);
-    }
-    acc = u;
+// K u = rhs with K = Lt D^2 Lt' (Lt unit lower in S.KL, D^-1 in S.dI): rhs in lane i (i < nd); returns u in
+// lane i, also stored to out[i].  Lt v = rhs, then Lt' u = D^-2 v.  The row and then the column of Lt a lane
+// needs are loaded up front (NP statically indexed registers); a step of either substitution is one readlane
+// broadcast and one fma, in blocks of 8 steps guarded by nd.
+template <int NP>
+__device__ __attribute__((noinline)) double chol_solve(const HS& S, int ls, int nd, double rhs, ldouble* out,
+                                                       int lane) {
+    const bool live = lane < nd;
+    const double di = live ? S.dI[lane] : 0.0;
+    double lr[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) lr[k] = (live && k < lane) ? S.KL[lane * ls + k] : 0.0;  // row lane of Lt
+    double acc = live ? rhs : 0.0, v = 0.0;
+#pragma unroll
+    for (int k0 = 0; k0 < NP; k0 += 8)
+        if (k0 < nd) {
+#pragma unroll
+            for (int k = k0; k < k0 + 8; ++k) {  // Lt v = rhs
+                const double vk = readlane_f64(acc, k);
+                v = lane == k ? vk : v;
+                acc = fma(-lr[k], vk, acc);
+            }
+        }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) lr[k] = (live && k > lane && k < nd) ? S.KL[k * ls + lane] : 0.0;  // column
+    acc = v * di * di;
     double sol = 0.0;
-    for (int k = nd - 1; k >= 0; --k) {  // L' u = w
-        const double lki = lane < k ? S.KL[k * ls + lane] : 0.0;
-        const double xk = readlane_f64(acc * di, k);
-        if (lane == k) sol = xk;
-        acc = fma(-lki, xk, acc);
-    }
-    if (lane < nd) out[lane] = sol;
+#pragma unroll
+    for (int k1 = NP; k1 > 0; k1 -= 8)
+        if (k1 - 8 < nd) {
+#pragma unroll
+            for (int k = k1 - 1; k >= k1 - 8; --k) {  // Lt' u = D^-2 v
+                const double xk = readlane_f64(acc, k);
+                sol = lane == k ? xk : sol;
+                acc = fma(-lr[k], xk, acc);
+            }
+        }
+    if (live) out[lane] = sol;
     LMPC_SYNC();
     return sol;
 }
 
-// t = R_r . vec (row r, nd columns)
-__device__ __forceinline__ double row_dot(const HS& S, int ls, int nd, int r, const ldouble* vec) {
-    double a = 0.0;
-    for (int j = 0; j < nd; ++j) a = fma(S.R[r * ls + j], vec[j], a);
-    return a;
+// t = R_r . vec (row r, nd columns); loads issued eight at a time ahead of their fmas
+__device__ __attribute__((noinline)) double row_dot(const HS& S, int ls, int nd, int r, const ldouble* vec) {
+    double a0 = 0.0, a1 = 0.0;
+    int j = 0;
+    for (; j + 8 <= nd; j += 8) {
+        double rv[8], vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            rv[u] = S.R[r * ls + j + u];
+            vv[u] = vec[j + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            a0 = fma(rv[u], vv[u], a0);
+            a1 = fma(rv[u + 1], vv[u + 1], a1);
+        }
+    }
+    for (; j < nd; ++j) a0 = fma(S.R[r * ls + j], vec[j], a0);
+    return a0 + a1;
 }
 // (R' q)_j for lane j
-__device__ __forceinline__ double rt_dot(const HS& S, int ls, int nr, const ldouble* q, int lane) {
-    double a = 0.0;
-    for (int r = 0; r < nr; ++r) a = fma(S.R[r * ls + lane], q[r], a);
-    return a;
+__device__ __attribute__((noinline)) double rt_dot(const HS& S, int ls, int nr, const ldouble* q, int lane) {
+    double a0 = 0.0, a1 = 0.0;
+    int r = 0;
+    for (; r + 8 <= nr; r += 8) {
+        double rv[8], qv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            rv[u] = S.R[(r + u) * ls + lane];
+            qv[u] = q[r + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            a0 = fma(rv[u], qv[u], a0);
+            a1 = fma(rv[u + 1], qv[u + 1], a1);
+        }
+    }
+    for (; r < nr; ++r) a0 = fma(S.R[r * ls + lane], q[r], a0);
+    return a0 + a1;
+}
+// (Hy y)_j for lane j < nd (Hy in global scratch, np x np)
+__device__ __attribute__((noinline)) double hy_dot(const HoqpDev& P, const gdouble* Hg, const ldouble* y, int nd,
+                                                   int lane) {
+    double a0 = 0.0, a1 = 0.0;
+    int i = 0;
+    for (; i + 8 <= nd; i += 8) {
+        double hv[8], yv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            hv[u] = Hg[(int64_t)(i + u) * P.np + lane];
+            yv[u] = y[i + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            a0 = fma(hv[u], yv[u], a0);
+            a1 = fma(hv[u + 1], yv[u + 1], a1);
+        }
+    }
+    for (; i < nd; ++i) a0 = fma(Hg[(int64_t)i * P.np + lane], y[i], a0);
+    return a0 + a1;
 }
 
 // Eigen FullPivLU of G (m x nd in S.KL) and Z' = Z ker(G) into Zn (n x np); returns the new nd.
 // Restates Eigen/src/LU/FullPivLU.h (3.3): compute() and kernel_retval::evalTo (tests/test_hoqp_oracle.py
 // pins the CPU restatement, oracle/hoqp.py fullpivlu / fullpivlu_kernel, that this follows step by step).
-__device__ int fullpivlu_kernel(const HoqpDev& P, const HS& S, int m, int nd, const gdouble* Z, gdouble* Zn,
+__device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P, const HS& S, int m, int nd, const gdouble* Z, gdouble* Zn,
                                 int lane) {
     const int ls = hq_ls(P);
     const int size = m < nd ? m : nd;
@@ -363,6 +471,80 @@ __device__ int fullpivlu_kernel(const HoqpDev& P, const HS& S, int m, int nd, co
     return dimker;
 }
 
+// Level setup: G = A Z (into S.KL), c = G'(A x - b) (S.c), Hy = G'G + 1e-12 I (Hg, full symmetric np x np).
+__device__ __attribute__((noinline)) void level_setup(const HoqpDev& P, const HS& S, const double* rec, int l,
+                                                      int nd, const gdouble* Z, gdouble* Hg, int lane) {
+    const int ls = hq_ls(P), m = P.m[l];
+    if (lane < P.np) S.c[lane] = 0.0;
+    d4 acc[10];
+#pragma unroll
+    for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    if (m > 0) {
+        const double* A = lev_a(P, rec, l);
+        gemm_xz(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, S.KL, ls, lane);
+        if (lane < m) {
+            const double* ar = A + (int64_t)lane * P.n;
+            double a = -lev_b(P, rec, l)[lane];
+            for (int k = 0; k < P.n; ++k) a = fma(ar[k], S.x[k], a);
+            S.vb[lane] = a;
+        }
+        LMPC_SYNC();
+        if (lane < nd) {
+            double a = 0.0;
+            for (int i = 0; i < m; ++i) a = fma(S.KL[i * ls + lane], S.vb[i], a);
+            S.c[lane] = a;
+        }
+        sym_tiles(P, S.KL, ls, m, nullptr, acc, lane);
+    }
+    const int g = lane >> 4, cc = lane & 15;
+#pragma unroll
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J)
+            if (I < P.nt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * I + 4 * i + g, col = 16 * J + cc;
+                    double v = acc[tid(I, J)][i];
+                    if (row == col && row < nd) v += HQ_REG;
+                    Hg[(int64_t)row * P.np + col] = v;
+                    Hg[(int64_t)col * P.np + row] = v;
+                }
+            }
+}
+
+// K = Hy + R' diag(wh) R on the matrix cores (lower tiles) into S.KL.
+__device__ __attribute__((noinline)) void form_K(const HoqpDev& P, const HS& S, int nr, const gdouble* Hg, int lane) {
+    const int ls = hq_ls(P), g = lane >> 4, cc = lane & 15;
+    d4 acc[10];
+#pragma unroll
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+            acc[tid(I, J)] = d4{0.0, 0.0, 0.0, 0.0};
+            if (I < P.nt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[tid(I, J)][i] = Hg[(int64_t)(16 * I + 4 * i + g) * P.np + 16 * J + cc];
+            }
+        }
+    sym_tiles(P, S.R, ls, nr, S.wh, acc, lane);
+#pragma unroll
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J)
+            if (I < P.nt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) S.KL[(16 * I + 4 * i + g) * ls + 16 * J + cc] = acc[tid(I, J)][i];
+            }
+    LMPC_SYNC();
+}
+
+// Constraint rows R = [D_stack; D_l] Z (rows 0..nr-1 of S.R).
+__device__ __attribute__((noinline)) void build_rows(const HoqpDev& P, const HS& S, const double* rec, int l, int p,
+                                                     int nr, const gdouble* Z, int lane) {
+    gemm_xz(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
+}
+
 // Interior-point state of the level's rows, slot k = row lane + 64 k (rows < nr = p + s, own rows r >= p).
 struct Rows {
     double s1[2], z1[2], v[2];  // own rows: -v <= 0 with slack s1
@@ -372,6 +554,7 @@ struct Rows {
 
 }  // namespace
 
+template <int NP>
 __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const double* __restrict__ recs,
                                                        double* __restrict__ xout, double* __restrict__ wout,
                                                        int32_t* __restrict__ status, int32_t* __restrict__ iters,
@@ -394,54 +577,29 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     if (lane < P.np) S.x[lane] = 0.0;
     LMPC_GSYNC();
     int nd = P.n, p = 0, st = 0;
+    HSTAMP_DECL
+    HQSUB_DECL
     for (int l = 0; l < P.L; ++l) {
         const int m = P.m[l], s = P.s[l], nr = p + s;
         const gdouble* Z = zbuf[zc];
         // ---- setup: G = A Z into KL, A x - b, c = G'(A x - b), Hy = G'G + 1e-12 I ---------------
-        if (lane < P.np) S.c[lane] = 0.0;
-        d4 acc[10];
-#pragma unroll
-        for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-        if (m > 0) {
-            const double* A = lev_a(P, rec, l);
-            gemm_xz(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, S.KL, ls, lane);
-            if (lane < m) {
-                const double* ar = A + (int64_t)lane * P.n;
-                double a = -lev_b(P, rec, l)[lane];
-                for (int k = 0; k < P.n; ++k) a = fma(ar[k], S.x[k], a);
-                S.vb[lane] = a;
-            }
-            LMPC_SYNC();
-            if (lane < nd) {
-                double a = 0.0;
-                for (int i = 0; i < m; ++i) a = fma(S.KL[i * ls + lane], S.vb[i], a);
-                S.c[lane] = a;
-            }
-            sym_tiles(P, S.KL, ls, m, nullptr, acc, lane);
-        }
-        {  // Hy to global, full symmetric, 1e-12 on the diagonal of the live block
-            const int g = lane >> 4, cc = lane & 15;
-#pragma unroll
-            for (int I = 0; I < 4; ++I)
-#pragma unroll
-                for (int J = 0; J <= I; ++J)
-                    if (I < P.nt) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int row = 16 * I + 4 * i + g, col = 16 * J + cc;
-                            double v = acc[tid(I, J)][i];
-                            if (row == col && row < nd) v += HQ_REG;
-                            Hg[(int64_t)row * P.np + col] = v;
-                            Hg[(int64_t)col * P.np + row] = v;
-                        }
-                    }
-        }
+        level_setup(P, S, rec, l, nd, Z, Hg, lane);
         LMPC_GSYNC();
+        HSTAMP(0);
         // ---- next basis Z' = Z ker(G) (HoQp.cpp:147-156), before K reuses the buffer ----------------
         int nd_next = nd;
         if (m > 0) nd_next = fullpivlu_kernel(P, S, m, nd, Z, zbuf[zc ^ 1], lane);
+        HSTAMP(1);
         // ---- constraint rows R = [D_stack; D_l] Z and their bounds -----------------------------------
-        gemm_xz(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, ls, lane);
+        build_rows(P, S, rec, l, p, nr, Z, lane);
+        // A higher level's row that lies in the span of the equalities fixed since (its projection D Z is zero
+        // up to rounding) constrains no y: 0 <= h, with h at rounding level when the row was active.  It is
+        // dropped (R row zeroed, h = 1) rather than left to make the level infeasible by one ulp.
+        double zmax = 0.0;
+        if (lane < P.n)
+            for (int j = 0; j < nd; ++j) zmax = fmax(zmax, fabs(Z[(int64_t)lane * P.np + j]));
+        zmax = wave_max(zmax);
+        LMPC_SYNC();
         Rows W;
         double bmax = 0.0;
 #pragma unroll
@@ -454,9 +612,20 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             if (r < nr) {
                 double f;
                 const double* dr = cons_row(P, rec, l, p, r, f);
-                double a = f;
-                for (int j = 0; j < P.n; ++j) a = fma(-dr[j], S.x[j], a);
-                if (r < p) a += wo[r];  // frozen slack, stacked current-last (HoQp.cpp:141-142, :176-182)
+                double a = f, dmx = 0.0;
+                for (int j = 0; j < P.n; ++j) {
+                    a = fma(-dr[j], S.x[j], a);
+                    dmx = fmax(dmx, fabs(dr[j]));
+                }
+                if (r < p) {
+                    a += wo[r];  // frozen slack, stacked current-last (HoQp.cpp:141-142, :176-182)
+                    double rmx = 0.0;
+                    for (int j = 0; j < nd; ++j) rmx = fmax(rmx, fabs(S.R[r * ls + j]));
+                    if (rmx <= 1e-12 * dmx * zmax) {
+                        for (int j = 0; j < P.np; ++j) S.R[r * ls + j] = 0.0;
+                        a = 1.0;
+                    }
+                }
                 W.bd[k] = a;
                 bmax = fmax(bmax, fabs(a));
                 if (r < p) {
@@ -475,6 +644,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         LMPC_SYNC();
         const double scale = 1.0 + fmax(wave_max(lane < nd ? fabs(S.c[lane]) : 0.0), wave_max(bmax));
         const double mc = (double)(p + 2 * s);
+        HSTAMP(2);
         // ---- interior point --------------------------------------------------------------------------
         int it = 0;
         for (;; ++it) {
@@ -504,76 +674,64 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             double rdy = 0.0;
             if (lane < nd) {
                 double a = S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
-                for (int i = 0; i < nd; ++i) a = fma(Hg[(int64_t)i * P.np + lane], S.y[i], a);
+                a += hy_dot(P, Hg, S.y, nd, lane);
                 rdy = a;
                 res = fmax(res, fabs(a));
             }
             const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
             res = wave_max(res);
-            if ((mu <= P.tol_mu * scale && res <= P.tol_res * scale) || it >= P.max_iter) break;
+            HSTAMP(3);
+            // converged; or degenerate (rows whose slack and multiplier both vanish): complementarity 1e3 below
+            // its tolerance while the dual residual stalls within 1e3 of its own, where the huge weights z/s
+            // of those rows leave the Newton directions no more accurate than the iterate already is
+            if ((mu <= P.tol_mu * scale && res <= P.tol_res * scale) ||
+                (mu <= 1e-3 * P.tol_mu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter)
+                break;
             // weights and K = Hy + R' diag(wh) R
-            double w1[2], wg[2], dl[2];
-#pragma unroll
+            double w1[2], wg[2], dl[2], is1[2], isg[2], idl[2];  // weights and the reciprocals both Newton
+#pragma unroll                                                        // systems divide by
             for (int k = 0; k < 2; ++k) {
                 const int r = lane + 64 * k;
-                w1[k] = W.z1[k] / W.s1[k];
-                wg[k] = W.zg[k] / W.sg[k];
+                is1[k] = 1.0 / W.s1[k];
+                isg[k] = 1.0 / W.sg[k];
+                w1[k] = W.z1[k] * is1[k];
+                wg[k] = W.zg[k] * isg[k];
                 dl[k] = 1.0 + w1[k] + wg[k];
-                if (r < P.rmax) S.wh[r] = r >= nr ? 0.0 : (r < p ? wg[k] : wg[k] * (1.0 + w1[k]) / dl[k]);
-            }
-#pragma unroll
-            for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-            {
-                const int g = lane >> 4, cc = lane & 15;
-#pragma unroll
-                for (int I = 0; I < 4; ++I)
-#pragma unroll
-                    for (int J = 0; J <= I; ++J)
-                        if (I < P.nt) {
-#pragma unroll
-                            for (int i = 0; i < 4; ++i)
-                                acc[tid(I, J)][i] = Hg[(int64_t)(16 * I + 4 * i + g) * P.np + 16 * J + cc];
-                        }
+                idl[k] = 1.0 / dl[k];
+                if (r < P.rmax) S.wh[r] = r >= nr ? 0.0 : (r < p ? wg[k] : wg[k] * (1.0 + w1[k]) * idl[k]);
             }
             LMPC_SYNC();
-            sym_tiles(P, S.R, ls, nr, S.wh, acc, lane);
-            {
-                const int g = lane >> 4, cc = lane & 15;
-#pragma unroll
-                for (int I = 0; I < 4; ++I)
-#pragma unroll
-                    for (int J = 0; J <= I; ++J)
-                        if (I < P.nt) {
-#pragma unroll
-                            for (int i = 0; i < 4; ++i)
-                                S.KL[(16 * I + 4 * i + g) * ls + 16 * J + cc] = acc[tid(I, J)][i];
-                        }
-            }
-            LMPC_SYNC();
-            chol_floor(S, ls, nd, lane);
+            form_K(P, S, nr, Hg, lane);
+            HSTAMP(4);
+            chol_floor<NP>(S, ls, nd, lane);
+            HSTAMP(5);
             // Newton system for a complementarity target rc (per row): returns dy (lane j) and per-row
             // directions; dz = W C dx + (z r_p - rc)/s, (H + C'WC) dx = -r_d - C'(z r_p - rc)/s
             double ds1[2], dsg[2], dz1[2], dzg[2], dv[2];
             auto newton = [&](const double rc1[2], const double rcg[2]) {
+                HQSUB_START();
                 double rv[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int r = lane + 64 * k;
                     rv[k] = 0.0;
                     if (r < nr) {
-                        const double eg = (W.zg[k] * rpg[k] - rcg[k]) / W.sg[k];
+                        const double eg = (W.zg[k] * rpg[k] - rcg[k]) * isg[k];
                         if (r < p) {
                             S.q[r] = -eg;
                         } else {
-                            const double e1 = (W.z1[k] * rp1[k] - rc1[k]) / W.s1[k];
+                            const double e1 = (W.z1[k] * rp1[k] - rc1[k]) * is1[k];
                             rv[k] = -rdv[k] + e1 + eg;
-                            S.q[r] = -eg + wg[k] * rv[k] / dl[k];
+                            S.q[r] = -eg + wg[k] * rv[k] * idl[k];
                         }
                     }
                 }
                 LMPC_SYNC();
+                HQSUB(0);
                 const double rhs = lane < nd ? -rdy + rt_dot(S, ls, nr, S.q, lane) : 0.0;
-                chol_solve(S, ls, nd, rhs, S.dy, lane);
+                HQSUB(1);
+                chol_solve<NP>(S, ls, nd, rhs, S.dy, lane);
+                HQSUB(2);
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int r = lane + 64 * k;
@@ -582,15 +740,16 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                         const double td = row_dot(S, ls, nd, r, S.dy);
                         double cg = td;
                         if (r >= p) {
-                            dv[k] = (rv[k] + wg[k] * td) / dl[k];
+                            dv[k] = (rv[k] + wg[k] * td) * idl[k];
                             cg = td - dv[k];
                             ds1[k] = -rp1[k] + dv[k];
-                            dz1[k] = (-rc1[k] - W.z1[k] * ds1[k]) / W.s1[k];
+                            dz1[k] = (-rc1[k] - W.z1[k] * ds1[k]) * is1[k];
                         }
                         dsg[k] = -rpg[k] - cg;
-                        dzg[k] = (-rcg[k] - W.zg[k] * dsg[k]) / W.sg[k];
+                        dzg[k] = (-rcg[k] - W.zg[k] * dsg[k]) * isg[k];
                     }
                 }
+                HQSUB(3);
             };
             auto max_step = [&]() {
                 double a = 1.0;
@@ -616,6 +775,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             }
             newton(rc1, rcg);
             const double a_aff = max_step();
+            HQSUB(4);
             double ca = 0.0;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -632,8 +792,10 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 rc1[k] = W.s1[k] * W.z1[k] + ds1[k] * dz1[k] - sig;
                 rcg[k] = W.sg[k] * W.zg[k] + dsg[k] * dzg[k] - sig;
             }
+            HQSUB(5);
             newton(rc1, rcg);
             const double a = fmin(1.0, HQ_FRAC * max_step());
+            HQSUB(4);
             if (lane < nd) S.y[lane] += a * S.dy[lane];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -644,6 +806,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 W.zg[k] += a * dzg[k];
             }
             LMPC_SYNC();
+            HQSUB(6);
+            HSTAMP(6);
         }
         if (it >= P.max_iter) st = 1;
         if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it;
@@ -669,7 +833,9 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             nd = nd_next;
         }
         p = nr;
+        HSTAMP(7);
     }
+    HSTAMP_FLUSH(b);
     // non-finite result: zeros, LMPC_QP_NAN
     bool bad = false;
     for (int l = 0; l < P.L; ++l)
@@ -685,12 +851,43 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     if (status && lane == 0) status[b] = st;
 }
 
+#ifdef LMPC_STAMPS
+extern "C" int lmpc_debug_hoqp_stamps(unsigned long long* out, int n) {
+    if (n > 4096) n = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_hoqp_stamps), (size_t)n * 8 * sizeof(unsigned long long)) ==
+                   hipSuccess ? n : -1;
+}
+extern "C" int lmpc_debug_hoqp_substamps(unsigned long long* out, int n) {
+    if (n > 4096) n = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_hoqp_substamps), (size_t)n * 8 * sizeof(unsigned long long)) ==
+                   hipSuccess ? n : -1;
+}
+#endif
+
 hipError_t launch_hoqp(const HoqpDev& P, const double* rec, int batch, double* x, double* w, int32_t* status,
                        int32_t* iters, double* scratch, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     const size_t lds = hq_lds_doubles(P) * sizeof(double);
-    hipLaunchKernelGGL(lmpc_hoqp_kernel, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters, scratch,
-                       batch);
+    switch (P.np) {
+        case 16:
+            hipLaunchKernelGGL(lmpc_hoqp_kernel<16>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
+                               scratch, batch);
+            break;
+        case 32:
+            hipLaunchKernelGGL(lmpc_hoqp_kernel<32>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
+                               scratch, batch);
+            break;
+        case 48:
+            hipLaunchKernelGGL(lmpc_hoqp_kernel<48>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
+                               scratch, batch);
+            break;
+        case 64:
+            hipLaunchKernelGGL(lmpc_hoqp_kernel<64>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
+                               scratch, batch);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

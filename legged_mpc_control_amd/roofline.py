@@ -80,3 +80,32 @@ def gi_flop(H: int, steps: float) -> float:
 def qp_bytes(H: int) -> int:
     """HBM bytes per QP: record (33+12H doubles) + contact (4H) + GRF out (12H doubles) + status + iters."""
     return (33 + 12 * H) * 8 + 4 * H + 12 * H * 8 + 8
+
+
+def hoqp_level_flop(n: int, m: int, s: int, p: int, nd: int, rank: int, iters: float) -> float:
+    """Algorithmic flops of one hierarchical-QP level (lmpc_hoqp.hip), FMA = 2 flops:
+    n variables, m equality / s own inequality / p frozen higher rows, nd null-space coordinates on entry,
+    rank = rank(A Z), iters interior-point iterations.
+
+      setup      G = A Z (2 m n nd) + G'G (m nd^2, symmetric) + c (2 m nd) + constraint rows R = D Z
+                 (2 r n nd, r = p + s) and their bounds (2 r n)
+      FullPivLU  2 sum_k (m - k - 1)(nd - k - 1) over k < min(m, nd), kernel solve rank^2 (nd - rank),
+                 Z' = Z K (2 n rank (nd - rank))
+      iteration  K = Hy + R' W R (r nd^2, symmetric) + Cholesky nd^3 / 3 + two solves (2 x 2 nd^2)
+                 + residuals R y, R'z, Hy y (4 r nd + 2 nd^2) + two Newton systems' R'q and R dy (8 r nd)
+      output     x += Z y (2 n nd) + slacks (2 s nd)
+    """
+    r = p + s
+    k = min(m, nd)
+    lu = 2.0 * sum((m - i - 1) * (nd - i - 1) for i in range(k)) if m else 0.0
+    dimker = nd - rank
+    setup = 2 * m * n * nd + m * nd * nd + 2 * m * nd + 2 * r * n * nd + 2 * r * n
+    basis = (lu + rank * rank * dimker + 2 * n * rank * dimker) if m else 0.0
+    it = r * nd * nd + nd ** 3 / 3 + 4 * nd * nd + 4 * r * nd + 2 * nd * nd + 8 * r * nd
+    return setup + basis + iters * it + 2 * n * nd + 2 * s * nd
+
+
+def hoqp_bytes(n: int, eq_rows, ineq_rows) -> int:
+    """HBM bytes of one instance: the record in (per level a, b, d, f) + x per level + slacks out."""
+    rec = sum((m + s) * (n + 1) for m, s in zip(eq_rows, ineq_rows))
+    return 8 * (rec + len(eq_rows) * n + sum(ineq_rows))

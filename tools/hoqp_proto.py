@@ -151,6 +151,12 @@ def hoqp_device(tasks, stats=None):
             c = np.zeros(nd)
         P = stk_d @ Z
         h = stk_f - stk_d @ x + stk_w
+        if P.shape[0]:  # dead frozen rows (lmpc_hoqp.hip): projection zero up to rounding
+            zmax = np.max(np.abs(Z))
+            dead = np.max(np.abs(P), axis=1) <= 1e-12 * np.max(np.abs(stk_d), axis=1) * zmax
+            P = P.copy(); h = h.copy()
+            P[dead] = 0.0
+            h[dead] = 1.0
         Dz = d @ Z
         g = t.f - d @ x if d.shape[0] else np.zeros(0)
         y, v, _ = level_ipm(Hy, c, P, h, Dz, g, stats=stats)
