@@ -140,32 +140,39 @@ __device__ __forceinline__ const double* cons_row(const HoqpDev& P, const double
 // C[rows][0..np) = X Z on the matrix cores; X row r = xrow(r) (global, n entries), Z global n x np
 // (columns nd..np-1 zero).  A[m][k] comes from lane 16k+m, B[k][n] from lane 16k+n, C element (4i+g, c)
 // lands in register i of lane 16g+c.
-template <class RowFn>
-__device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, const gdouble* Z, ldouble* C, int ldc, int lane) {
+template <int NP, class RowFn>
+__device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, const gdouble* Z, ldouble* C, int ldc,
+                                        int lane) {
+    constexpr int KC = NP / 4, NT = NP / 16;  // k chunks of 4, column tiles
     const int kq = lane >> 4, mm = lane & 15;
+    double bz[KC][NT];  // this lane's B operands for every chunk and tile, loaded once for all row tiles
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+        const int k = 4 * c + kq;
+#pragma unroll
+        for (int J = 0; J < NT; ++J) bz[c][J] = k < P.n ? Z[(int64_t)k * P.np + 16 * J + mm] : 0.0;
+    }
     for (int I = 0; I * 16 < rows; ++I) {
         const double* xr = (16 * I + mm < rows) ? xrow(16 * I + mm) : nullptr;
-        d4 acc[4];
+        double a[KC];
 #pragma unroll
-        for (int J = 0; J < 4; ++J) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
-        for (int k0 = 0; k0 < P.n; k0 += 4) {
-            const int k = k0 + kq;
-            const double a = (xr != nullptr && k < P.n) ? xr[k] : 0.0;
-#pragma unroll
-            for (int J = 0; J < 4; ++J)
-                if (J < P.nt) {
-                    const double bz = k < P.n ? Z[(int64_t)k * P.np + 16 * J + mm] : 0.0;
-                    acc[J] = MFMA64(a, bz, acc[J]);
-                }
+        for (int c = 0; c < KC; ++c) {
+            const int k = 4 * c + kq;
+            a[c] = (xr != nullptr && k < P.n) ? xr[k] : 0.0;
         }
+        d4 acc[NT];
 #pragma unroll
-        for (int J = 0; J < 4; ++J)
-            if (J < P.nt) {
+        for (int J = 0; J < NT; ++J) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = 16 * I + 4 * i + kq;
-                    if (row < rows) C[row * ldc + 16 * J + mm] = acc[J][i];
-                }
+        for (int c = 0; c < KC; ++c)
+#pragma unroll
+            for (int J = 0; J < NT; ++J) acc[J] = MFMA64(a[c], bz[c][J], acc[J]);
+#pragma unroll
+        for (int J = 0; J < NT; ++J)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 16 * I + 4 * i + kq;
+                if (row < rows) C[row * ldc + 16 * J + mm] = acc[J][i];
             }
     }
 }
@@ -392,7 +399,18 @@ __device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P, cons
         if (lane > k && lane < m) {
             const double l = S.KL[lane * ls + k] / pk;
             S.KL[lane * ls + k] = l;
-            for (int j = k + 1; j < nd; ++j) S.KL[lane * ls + j] -= l * S.KL[k * ls + j];
+            int j = k + 1;
+            for (; j + 8 <= nd; j += 8) {  // loads of a block ahead of its updates
+                double a[8], u[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    a[t] = S.KL[lane * ls + j + t];
+                    u[t] = S.KL[k * ls + j + t];
+                }
+#pragma unroll
+                for (int t = 0; t < 8; ++t) S.KL[lane * ls + j + t] = a[t] - l * u[t];
+            }
+            for (; j < nd; ++j) S.KL[lane * ls + j] -= l * S.KL[k * ls + j];
         }
         LMPC_SYNC();
     }
@@ -456,22 +474,68 @@ __device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P, cons
         }
         LMPC_SYNC();
     }
-    // basis K: row Q[i] = -M[i] (i < rank), row Q[rank + k] = e_k;  Z' = Z K, lane = row of Z
-    if (lane < P.n) {
-        const gdouble* zr = Z + (int64_t)lane * P.np;
-        for (int cc = 0; cc < P.np; ++cc) {
-            double a = 0.0;
-            if (cc < dimker) {
-                a = zr[S.qp[rank + cc]];
-                for (int i = 0; i < rank; ++i) a -= zr[S.qp[i]] * S.KL[i * ls + rank + cc];
-            }
-            Zn[(int64_t)lane * P.np + cc] = a;
+    // basis K (nd x dimker): row Q[i] = -M[i] (i < rank), row Q[rank + k] = e_k.  Z' = Z K on the matrix cores,
+    // K's entries generated from M and the inverse permutation (S.rt reused: qinv[j] = position of j in Q)
+    if (lane < nd) S.rt[S.qp[lane]] = lane;
+    LMPC_SYNC();
+    const int kq = lane >> 4, mm = lane & 15;
+    for (int I = 0; I * 16 < P.n; ++I) {
+        const int zrow = 16 * I + mm;
+        d4 acc[4];
+#pragma unroll
+        for (int J = 0; J < 4; ++J) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < nd; k0 += 4) {
+            const int j = k0 + kq;
+            const double a = (zrow < P.n && j < nd) ? Z[(int64_t)zrow * P.np + j] : 0.0;
+            const int qi = j < nd ? S.rt[j] : -1;
+#pragma unroll
+            for (int J = 0; J < 4; ++J)
+                if (J < P.nt) {
+                    const int c = 16 * J + mm;
+                    double bk = 0.0;
+                    if (qi >= 0 && c < dimker) bk = qi < rank ? -S.KL[qi * ls + rank + c] : (qi - rank == c ? 1.0 : 0.0);
+                    acc[J] = MFMA64(a, bk, acc[J]);
+                }
         }
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+            if (J < P.nt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * I + 4 * i + kq;
+                    if (row < P.n) Zn[(int64_t)row * P.np + 16 * J + mm] = acc[J][i];
+                }
+            }
     }
     return dimker;
 }
 
+// g . x over n entries of a global row (per-lane rows: uncoalesced), loads issued eight at a time ahead of their
+// fmas; amax = max |g_j|
+__device__ __forceinline__ double gdot(const double* g, const ldouble* x, int n, double& amax) {
+    double a0 = 0.0, a1 = 0.0, mx = 0.0;
+    int j = 0;
+    for (; j + 8 <= n; j += 8) {
+        double gv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gv[u] = g[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            a0 = fma(gv[u], x[j + u], a0);
+            a1 = fma(gv[u + 1], x[j + u + 1], a1);
+            mx = fmax(mx, fmax(fabs(gv[u]), fabs(gv[u + 1])));
+        }
+    }
+    for (; j < n; ++j) {
+        a0 = fma(g[j], x[j], a0);
+        mx = fmax(mx, fabs(g[j]));
+    }
+    amax = mx;
+    return a0 + a1;
+}
+
 // Level setup: G = A Z (into S.KL), c = G'(A x - b) (S.c), Hy = G'G + 1e-12 I (Hg, full symmetric np x np).
+template <int NP>
 __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P, const HS& S, const double* rec, int l,
                                                       int nd, const gdouble* Z, gdouble* Hg, int lane) {
     const int ls = hq_ls(P), m = P.m[l];
@@ -481,12 +545,10 @@ __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P, const HS
     for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     if (m > 0) {
         const double* A = lev_a(P, rec, l);
-        gemm_xz(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, S.KL, ls, lane);
+        gemm_xz<NP>(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, S.KL, ls, lane);
         if (lane < m) {
-            const double* ar = A + (int64_t)lane * P.n;
-            double a = -lev_b(P, rec, l)[lane];
-            for (int k = 0; k < P.n; ++k) a = fma(ar[k], S.x[k], a);
-            S.vb[lane] = a;
+            double amx;
+            S.vb[lane] = gdot(A + (int64_t)lane * P.n, S.x, P.n, amx) - lev_b(P, rec, l)[lane];
         }
         LMPC_SYNC();
         if (lane < nd) {
@@ -540,9 +602,10 @@ __device__ __attribute__((noinline)) void form_K(const HoqpDev& P, const HS& S, 
 }
 
 // Constraint rows R = [D_stack; D_l] Z (rows 0..nr-1 of S.R).
+template <int NP>
 __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P, const HS& S, const double* rec, int l, int p,
                                                      int nr, const gdouble* Z, int lane) {
-    gemm_xz(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
+    gemm_xz<NP>(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
 }
 
 // Interior-point state of the level's rows, slot k = row lane + 64 k (rows < nr = p + s, own rows r >= p).
@@ -583,7 +646,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         const int m = P.m[l], s = P.s[l], nr = p + s;
         const gdouble* Z = zbuf[zc];
         // ---- setup: G = A Z into KL, A x - b, c = G'(A x - b), Hy = G'G + 1e-12 I ---------------
-        level_setup(P, S, rec, l, nd, Z, Hg, lane);
+        level_setup<NP>(P, S, rec, l, nd, Z, Hg, lane);
         LMPC_GSYNC();
         HSTAMP(0);
         // ---- next basis Z' = Z ker(G) (HoQp.cpp:147-156), before K reuses the buffer ----------------
@@ -591,7 +654,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         if (m > 0) nd_next = fullpivlu_kernel(P, S, m, nd, Z, zbuf[zc ^ 1], lane);
         HSTAMP(1);
         // ---- constraint rows R = [D_stack; D_l] Z and their bounds -----------------------------------
-        build_rows(P, S, rec, l, p, nr, Z, lane);
+        build_rows<NP>(P, S, rec, l, p, nr, Z, lane);
         // A higher level's row that lies in the span of the equalities fixed since (its projection D Z is zero
         // up to rounding) constrains no y: 0 <= h, with h at rounding level when the row was active.  It is
         // dropped (R row zeroed, h = 1) rather than left to make the level infeasible by one ulp.
@@ -612,11 +675,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             if (r < nr) {
                 double f;
                 const double* dr = cons_row(P, rec, l, p, r, f);
-                double a = f, dmx = 0.0;
-                for (int j = 0; j < P.n; ++j) {
-                    a = fma(-dr[j], S.x[j], a);
-                    dmx = fmax(dmx, fabs(dr[j]));
-                }
+                double dmx;
+                double a = f - gdot(dr, S.x, P.n, dmx);
                 if (r < p) {
                     a += wo[r];  // frozen slack, stacked current-last (HoQp.cpp:141-142, :176-182)
                     double rmx = 0.0;
