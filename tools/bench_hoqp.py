@@ -154,6 +154,12 @@ def main():
     err_w = D.max_over_ranks(err_w, dist, dev)
     stats = D.sum_over_ranks([(st == 0).sum(), (st == 1).sum(), (st == 2).sum()], dist, dev)
 
+    traffic = None  # HBM bytes per launch from the committed PMC passes (tools/profile_hoqp.sh)
+    try:
+        tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["wbc_hoqp_3level_n42"]
+        traffic = tr["bytes_per_qp"] * B
+    except (OSError, ValueError, KeyError):
+        traffic = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         t1 = time.perf_counter()
@@ -193,7 +199,7 @@ def main():
                 "peak": roofline.FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / roofline.FP64_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
                 "kernel": "lmpc_hoqp_kernel",
                 "kernel_ms": kernel_ms,
                 "flop_per_instance": flop_per,

@@ -31,7 +31,35 @@ def per_kernel(name, kern):
     return [float(x["Counter_Value"]) for x in r], [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in r]
 
 
+def main_hoqp():
+    """tools/profile_hoqp.sh output (gpurun_out/prof_hoqp) -> profiles/<tag>/hoqp_kernel_stats.csv,
+    hoqp_pmc_per_dispatch.json and profiles/pmc_traffic.json["wbc_hoqp_3level_n42"]."""
+    global SRC
+    SRC = os.path.join(ROOT, "gpurun_out", "prof_hoqp")
+    os.makedirs(DST, exist_ok=True)
+    cal = json.load(open(os.path.join(DST, "pmc_calibration.json")))
+    rf, wf = cal["read_factor"], cal["write_factor"]
+    f, fd = per_kernel("fhq", "lmpc_hoqp_kernel")
+    w, wd = per_kernel("whq", "lmpc_hoqp_kernel")
+    fb, wb = st.mean(f) * 1024 * rf, st.mean(w) * 1024 * wf
+    B = 4096
+    json.dump(dict(fetch_kib_raw=f, write_kib_raw=w, fetch_bytes=fb, write_bytes=wb, dispatch_ns_fetch_pass=fd,
+                   dispatch_ns_write_pass=wd), open(os.path.join(DST, "hoqp_pmc_per_dispatch.json"), "w"), indent=1)
+    traffic = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    traffic["wbc_hoqp_3level_n42"] = {
+        "bytes_per_launch": fb + wb, "bytes_per_qp": (fb + wb) / B, "fetch_bytes": fb, "write_bytes": wb,
+        "source": f"profiles/{TAG}/hoqp_pmc_per_dispatch.json",
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of tools/bench_hoqp.py "
+                  f"(B = {B}); FETCH_SIZE x {rf:.3f}, WRITE_SIZE x {wf:.3f} from profiles/{TAG}/pmc_calibration.json"}
+    json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    shutil.copy(os.path.join(SRC, "hq", "hq_kernel_stats.csv"), os.path.join(DST, "hoqp_kernel_stats.csv"))
+    shutil.copy(os.path.join(SRC, "hq_bench.log"), os.path.join(DST, "hoqp_prof_bench.log"))
+    print("wbc_hoqp_3level_n42", round((fb + wb) / 1e6, 1), "MB/launch", round((fb + wb) / B), "B/hierarchy")
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[2] == "hoqp":
+        return main_hoqp()
     os.makedirs(DST, exist_ok=True)
     cal = {}
     for tag, ctr in (("calf", "FETCH_SIZE"), ("calw", "WRITE_SIZE")):
