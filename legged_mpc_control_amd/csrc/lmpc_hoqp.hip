@@ -707,6 +707,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         HSTAMP(2);
         // ---- interior point --------------------------------------------------------------------------
         int it = 0;
+        bool numstop = false;  // left on a non-finite Newton direction
+        double mu_last = 0.0;
         for (;; ++it) {
             // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
             double rp1[2], rpg[2], rdv[2];
@@ -739,6 +741,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 res = fmax(res, fabs(a));
             }
             const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
+            mu_last = mu;
             res = wave_max(res);
             HSTAMP(3);
             // converged; or degenerate (rows whose slack and multiplier both vanish): complementarity 1e3 below
@@ -856,6 +859,17 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             newton(rc1, rcg);
             const double a = fmin(1.0, HQ_FRAC * max_step());
             HQSUB(4);
+            // a non-finite direction (weights z/s overflowing as a degenerate level's slacks reach the bottom
+            // of the double range) ends the level on the current iterate, which is kept
+            bool fin = isfinite(a) && (lane >= nd || isfinite((double)S.dy[lane]));
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                fin = fin && isfinite(dv[k]) && isfinite(ds1[k]) && isfinite(dz1[k]) && isfinite(dsg[k]) &&
+                      isfinite(dzg[k]);
+            if (__ballot(!fin)) {
+                numstop = true;
+                break;
+            }
             if (lane < nd) S.y[lane] += a * S.dy[lane];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -869,7 +883,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             HQSUB(6);
             HSTAMP(6);
         }
-        if (it >= P.max_iter) st = 1;
+        if (it >= P.max_iter || (numstop && mu_last > 1e3 * P.tol_mu * scale)) st = 1;
         if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it;
         // ---- outputs: w_l = max(0, D_l Z y - g) for the final y, x += Z y ------------------------------
 #pragma unroll

@@ -8,6 +8,9 @@ Groups (each one batch of same-shaped hierarchies, packed as include/lmpc/lmpc_h
            the last level, so its x is comparable across solvers;
   rand3 -- random three-level hierarchies over 8 variables with inequalities on levels 0-2 (the draws the
            reference's slack pairing leaves feasible, HoQp.cpp:58 vs :176-182);
+  n20 / n64 -- random chains over 20 and 64 variables (the kernel's 32- and 64-wide tile instances; n64 has four
+           levels), pinned by their last level;
+  exhaust -- chains whose second level leaves no null space (Eigen's single zero kernel column afterwards);
   ref   -- the reference's own test data (src/test/ho_qp_test.cpp:10-22, regenerated bit for bit).
 Expected values come from oracle/hoqp.py (exact primal active set in x87 extended precision, Eigen's
 FullPivLU kernel basis); every level is certified by its KKT conditions here, and the wbc group's levels
@@ -102,11 +105,33 @@ def main():
         seed += 1
     out.update({f"rand3_{k}": v for k, v in group(rand, False).items()})
     out["rand3_infeasible_seeds"] = np.array(infeasible, dtype=np.int32)
+    # the kernel's other tile widths and shapes: n = 20 (np 32), n = 64 (np 64, four levels), and a chain whose
+    # second level exhausts the null space (Eigen's single zero kernel column for the levels after it)
+    def feasible_group(name, make, count, pinned):
+        chains, seed = [], 0
+        while len(chains) < count:
+            c = make(np.random.default_rng(5000 + 100 * len(name) + seed))
+            seed += 1
+            try:
+                oracle_chain(c)
+                chains.append(c)
+            except ValueError:
+                pass
+        out.update({f"{name}_{k}": v for k, v in group(chains, pinned).items()})
+        return len(chains)
+
+    feasible_group("n20", lambda r: [random_task(r, 20, 6, 10, True), random_task(r, 20, 5, 6, False),
+                                     random_task(r, 20, 9, 0, False)], 6, True)
+    feasible_group("n64", lambda r: [random_task(r, 64, 20, 30, True), random_task(r, 64, 16, 10, False),
+                                     random_task(r, 64, 16, 0, False), random_task(r, 64, 20, 0, False)], 3, True)
+    feasible_group("exhaust", lambda r: [random_task(r, 6, 2, 3, True), random_task(r, 6, 4, 2, False),
+                                         random_task(r, 6, 2, 2, False)], 6, True)
     t0, t1 = Q.reference_test_tasks()
     ref = [HQ.Task(t0.a, t0.b, t0.d, t0.f), HQ.Task(t1.a, t1.b, t1.d, t1.f)]
     out.update({f"ref_{k}": v for k, v in group([ref], False).items()})
     np.savez_compressed(OUT, **out)
-    print(f"wrote {OUT}: wbc {len(wbc)}, rand3 {len(rand)} (quirk-infeasible seeds {infeasible[:5]}...), ref 1")
+    print(f"wrote {OUT}: wbc {len(wbc)}, rand3 {len(rand)} (quirk-infeasible seeds {infeasible[:5]}...), n20, n64, "
+          f"exhaust, ref 1")
 
 
 if __name__ == "__main__":

@@ -45,7 +45,7 @@ def unpack(rec, dims):
     return out
 
 
-def check_against(rec, dims, x, w, x_ref, w_ref, pinned):
+def check_against(rec, dims, x, w, x_ref, w_ref, pinned, TOL=TOL):
     levels = unpack(rec, dims)
     scale = 1.0 + max(float(np.max(np.abs(rec))), float(np.max(np.abs(x_ref))))
     for l, (a, b, d, f) in enumerate(levels):
@@ -80,7 +80,7 @@ def hq():
     return hoqp
 
 
-@pytest.mark.parametrize("group", ["wbc", "rand3", "ref"])
+@pytest.mark.parametrize("group", ["wbc", "rand3", "n20", "n64", "exhaust", "ref"])
 def test_golden_groups(hq, group):
     g = load(group)
     dims = dims_from(g["dims"])
@@ -89,8 +89,12 @@ def test_golden_groups(hq, group):
     x, w, st, it = solver.solve(g["rec"])
     assert np.all(st == 0), st
     assert np.all((it > 0) & (it < 60))
+    # n64: four dense random levels over 64 variables with 20+ active rows each.  On such degenerate levels the
+    # interior point stops where its dual residual stalls, ~1e-4 of the data scale away from the exact active-set
+    # answer along flat directions ("Accuracy"); the WBC and the other groups meet 1e-6.
+    tol = 2e-4 if group == "n64" else TOL
     for b in range(B):
-        check_against(g["rec"][b], dims, x[b], w[b], g["x"][b], g["w"][b], bool(g["pinned"]))
+        check_against(g["rec"][b], dims, x[b], w[b], g["x"][b], g["w"][b], bool(g["pinned"]), tol)
 
 
 def test_reference_two_task_checks(hq):

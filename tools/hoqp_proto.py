@@ -48,17 +48,62 @@ def chol_solve(L, r):
     return x
 
 
+def polish(Hy, c, P, h, Dz, g, y_ipm, s2, z2, s3, z3, scale, rounds=3):
+    """Active-set refinement after the interior point (kernel plan): frozen rows with z > s held by an augmented
+    Lagrangian (weight rho, multipliers from the IPM's z), own rows with z > s kept as 1/2 (d y - g)^2; the
+    result is kept only if it verifies (feasible, consistent classification, nonnegative multipliers)."""
+    p, s = P.shape[0], Dz.shape[0]
+    actP = z2 > s2 if p else np.zeros(0, bool)
+    slk = z3 > s3 if s else np.zeros(0, bool)
+    dmax = max(1.0, float(np.max(np.diag(Hy))))
+    rho = float(os.environ.get("RHO", 1e6)) * dmax
+    K = Hy.copy()
+    if s:
+        K += Dz[slk].T @ Dz[slk]
+    if p:
+        K += rho * P[actP].T @ P[actP]
+    L = chol_floor(K)
+    lam = z2.copy() if p else np.zeros(0)
+    y = y_ipm
+    for _ in range(rounds):
+        rhs = -c.copy()
+        if s:
+            rhs += Dz[slk].T @ g[slk]
+        if p:
+            rhs += P[actP].T @ (rho * h[actP] - lam[actP])
+        y = chol_solve(L, rhs)
+        if p:
+            lam[actP] += rho * (P[actP] @ y - h[actP])
+    tp = 1e-9 * scale
+    ok = True
+    if p:
+        ok &= bool(np.all(P @ y <= h + tp)) and bool(np.all(lam[actP] >= -tp))
+    if s:
+        r = Dz @ y - g
+        ok &= bool(np.all(r[slk] >= -tp)) and bool(np.all(r[~slk] <= tp))
+    POLISH_STATS.append(ok)
+    return y if ok else y_ipm
+
+
+POLISH_STATS = []
+
+
 def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1e-13)), frac=0.99, stats=None):
     """min 1/2 y'Hy y + c'y + 1/2 v'v  s.t. -v <= 0, P y <= h, Dz y - v <= g.  Returns (y, v, iters)."""
     nd, p, s = Hy.shape[0], P.shape[0], Dz.shape[0]
     m = 2 * s + p
+    init = os.environ.get("INIT", "zero")
     y = np.zeros(nd)
-    v = np.maximum(0.0, -g) + 1.0 if s else np.zeros(0)
-    # slacks of the three blocks; start them (and the duals) at least at 1
-    s1 = np.maximum(v, 1.0)
-    s2 = np.maximum(h - P @ y, 1.0) if p else np.zeros(0)
-    s3 = np.maximum(g - Dz @ y + v, 1.0) if s else np.zeros(0)
-    z1, z2, z3 = np.ones(s), np.ones(p), np.ones(s)
+    if init.startswith("ls"):  # unconstrained minimiser of the level objective
+        y = chol_solve(chol_floor(Hy), -c)
+    floor = float(os.environ.get("SFLOOR", 1.0))
+    v = np.maximum(0.0, (Dz @ y - g) if s else 0.0) + floor if s else np.zeros(0)
+    # slacks of the three blocks; start them (and the duals) at least at the floor
+    s1 = np.maximum(v, floor)
+    s2 = np.maximum(h - P @ y, floor) if p else np.zeros(0)
+    s3 = np.maximum(g - Dz @ y + v, floor) if s else np.zeros(0)
+    z0 = float(os.environ.get("Z0", 1.0))
+    z1, z2, z3 = z0 * np.ones(s), z0 * np.ones(p), z0 * np.ones(s)
     scale = 1.0 + max(np.max(np.abs(c)) if nd else 0.0, np.max(np.abs(h)) if p else 0.0,
                       np.max(np.abs(g)) if s else 0.0)
     it = 0
@@ -74,7 +119,8 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
         mu = sig @ zz / m if m else 0.0
         res = max(np.max(np.abs(rdy)) if nd else 0.0, np.max(np.abs(rdv)) if s else 0.0,
                   np.max(np.abs(np.concatenate([rp1, rp2, rp3]))) if m else 0.0)
-        if mu <= tol * scale and res <= float(os.environ.get('RTOL', 1e-10)) * scale:
+        rtol = float(os.environ.get('RTOL', 1e-10))
+        if (mu <= tol * scale and res <= rtol * scale) or (mu <= float(os.environ.get('STALL_MU', 1e-16)) * scale and res <= 1e3 * rtol * scale):
             break
         w1, w2, w3 = z1 / s1, z2 / s2, z3 / s3
         dlt = 1.0 + w1 + w3
@@ -122,6 +168,8 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
         z1, z2, z3 = z1 + a * dz2_[0], z2 + a * dz2_[1], z3 + a * dz2_[2]
     if stats is not None:
         stats.append(it)
+    if os.environ.get("POLISH"):
+        y = polish(Hy, c, P, h, Dz, g, y, s2, z2, s3, z3, scale)
     if s and os.environ.get("VEXACT"):
         v = np.maximum(0.0, Dz @ y - g)
     if os.environ.get("VERBOSE"):
