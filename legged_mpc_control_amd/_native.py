@@ -41,7 +41,7 @@ ABI_VERSION = 4
 HOQP_SYMBOLS = (
     "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
     "lmpc_hoqp_create", "lmpc_hoqp_destroy", "lmpc_hoqp_set_options", "lmpc_hoqp_solve_batch",
-    "lmpc_hoqp_solve_device", "lmpc_hoqp_sync",
+    "lmpc_hoqp_solve_device", "lmpc_hoqp_sync", "lmpc_wbc_tasks", "lmpc_wbc_tasks_device",
 )
 HOQP_MAX_LEVELS = 4
 
@@ -125,6 +125,15 @@ class LmpcHoqpDims(ctypes.Structure):
 
 class LmpcHoqpOptions(ctypes.Structure):
     _fields_ = [("max_iter", ctypes.c_int32), ("tol_mu", ctypes.c_double), ("tol_res", ctypes.c_double)]
+
+
+class LmpcWbcInput(ctypes.Structure):
+    _fields_ = [
+        ("M", ctypes.c_double * 324), ("nle", ctypes.c_double * 18), ("J", ctypes.c_double * 216),
+        ("dJv", ctypes.c_double * 12), ("base_accel", ctypes.c_double * 6), ("swing_acc", ctypes.c_double * 12),
+        ("forces_des", ctypes.c_double * 12), ("torque_limits", ctypes.c_double * 3), ("mu", ctypes.c_double),
+        ("contact", ctypes.c_int32 * 4),
+    ]
 
 
 class NativeLibraryError(RuntimeError):
@@ -246,6 +255,10 @@ def lib():
         L.lmpc_hoqp_solve_device.restype = ctypes.c_int
         L.lmpc_hoqp_sync.argtypes = [vp]
         L.lmpc_hoqp_sync.restype = ctypes.c_int
+        L.lmpc_wbc_tasks.argtypes = [ctypes.POINTER(LmpcWbcInput), dp]
+        L.lmpc_wbc_tasks.restype = ctypes.c_int
+        L.lmpc_wbc_tasks_device.argtypes = [vp, ctypes.c_int, vp, vp]
+        L.lmpc_wbc_tasks_device.restype = ctypes.c_int
         if L.lmpc_abi_version() != ABI_VERSION:
             raise NativeLibraryError("liblmpc.so ABI version mismatch")
         _lib = L

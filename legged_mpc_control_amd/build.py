@@ -16,7 +16,7 @@ ARCH = "gfx950"
 # config 2 0.342 -> 0.329 ms, config 4 22.4 -> 22.0 ms (profiles/r02/diag_ab_configs.log).
 HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 
-SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_capi.cpp",
+SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
            "hoqp_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
 HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_hoqp_device.h"]
 

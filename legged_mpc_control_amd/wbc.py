@@ -151,3 +151,55 @@ def synth_wbc_tasks(seed: int, padded=True):
     s = synth_wbc(seed)
     return wbc_tasks(s["M"], s["nle"], s["J"], s["dJv"], s["contact"], s["base_accel"], s["swing_acc"],
                      s["forces_des"], padded=padded)
+
+
+def wbc_input(M, nle, J, dJv, contact, base_accel, swing_acc, forces_des, torque_limits=TORQUE_LIMITS,
+              mu=FRICTION_COEFF):
+    """The C-ABI's per-robot input block (include/lmpc/lmpc_hoqp.h lmpc_wbc_input)."""
+    from ._native import LmpcWbcInput
+
+    s = LmpcWbcInput()
+    s.M[:] = list(np.asarray(M, dtype=np.float64).reshape(-1))
+    s.nle[:] = list(np.asarray(nle, dtype=np.float64))
+    s.J[:] = list(np.asarray(J, dtype=np.float64).reshape(-1))
+    s.dJv[:] = list(np.asarray(dJv, dtype=np.float64))
+    s.base_accel[:] = list(np.asarray(base_accel, dtype=np.float64))
+    s.swing_acc[:] = list(np.asarray(swing_acc, dtype=np.float64).reshape(-1))
+    s.forces_des[:] = list(np.asarray(forces_des, dtype=np.float64))
+    s.torque_limits[:] = list(np.asarray(torque_limits, dtype=np.float64))
+    s.mu = float(mu)
+    s.contact[:] = [int(bool(c)) for c in contact]
+    return s
+
+
+def record_native(inp) -> np.ndarray:
+    """One WBC record by the product's host restatement (lmpc_wbc_tasks)."""
+    import ctypes
+
+    from ._native import check, lib
+
+    rec = np.zeros(4472)
+    check(lib().lmpc_wbc_tasks(ctypes.byref(inp), rec.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
+          "lmpc_wbc_tasks")
+    return rec
+
+
+def records_device(d_inputs, d_records, stream=None):
+    """A batch of WBC records on the device (lmpc_wbc_tasks_device): d_inputs = uint8 torch tensor [B][sizeof
+    lmpc_wbc_input] in HBM, d_records = float64 [B][4472]."""
+    import ctypes
+
+    import torch
+
+    from ._native import check, lib
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    check(lib().lmpc_wbc_tasks_device(ctypes.c_void_p(d_inputs.data_ptr()), d_inputs.shape[0],
+                                      ctypes.c_void_p(d_records.data_ptr()), ctypes.c_void_p(s.cuda_stream)),
+          "lmpc_wbc_tasks_device")
+
+
+def synth_input(seed: int):
+    s = synth_wbc(seed)
+    return wbc_input(s["M"], s["nle"], s["J"], s["dJv"], s["contact"], s["base_accel"], s["swing_acc"],
+                     s["forces_des"])

@@ -146,3 +146,19 @@ def test_golden_fixture_is_certified():
     assert np.allclose(d["ref_x"][0, 1], h1.solution(), atol=1e-12)
     assert np.allclose(d["ref_w"][0], h1.stacked_slack, atol=1e-12)
     assert d["wbc_rec"].shape == (16, 4472) and bool(d["wbc_pinned"])
+
+
+def test_wbc_task_assembly_native_matches_formulation():
+    """lmpc_wbc_tasks (C, the device kernel's restatement) == wbc.wbc_tasks packed, bitwise, for every one of
+    the 16 contact patterns (flight and single-leg stance included) on synthetic dynamics."""
+    assert ctypes.sizeof(N.LmpcWbcInput) == 4848
+    s = W.synth_wbc(3)
+    for mask in range(16):
+        contact = [(mask >> i) & 1 for i in range(4)]
+        tasks = W.wbc_tasks(s["M"], s["nle"], s["J"], s["dJv"], contact, s["base_accel"], s["swing_acc"],
+                            s["forces_des"])
+        rec = HQ.pack(tasks, HQ.dims_of(tasks))
+        nat = W.record_native(W.wbc_input(s["M"], s["nle"], s["J"], s["dJv"], contact, s["base_accel"],
+                                          s["swing_acc"], s["forces_des"]))
+        assert np.array_equal(rec, nat), (mask, np.nonzero(rec != nat)[0][:8])
+    assert N.lib().lmpc_wbc_tasks(None, None) == -1
