@@ -93,6 +93,20 @@ def build_cpp_test(force: bool = False) -> str:
     return out
 
 
+def build_cpp_hoqp_test(force: bool = False) -> str:
+    """C++ program running the reference's HoQp test (ho_qp_test.cpp) against legged::HoQp (include/lmpc/HoQp.hpp)."""
+    src = os.path.join(ROOT, "tests", "cpp", "ho_qp_test.cpp")
+    out = os.path.join(ROOT, "tests", "cpp", "build", "ho_qp_test")
+    hdr = os.path.join(ROOT, "include", "lmpc", "HoQp.hpp")
+    if not force and not _stale(out, [src, hdr, LIB]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", out, src,
+           "-L", LIBDIR, "-llmpc", f"-Wl,-rpath,{LIBDIR}"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_tool_cpp(name: str, force: bool = False) -> str:
     """Dev tool program over liblmpc.so (tools/<name>.cpp -> tools/build/<name>); never shipped."""
     src = os.path.join(ROOT, "tools", f"{name}.cpp")

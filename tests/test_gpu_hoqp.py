@@ -216,3 +216,14 @@ def test_wbc_tasks_on_device_then_solve(hq):
     torch.cuda.synchronize()
     assert np.array_equal(d_x.cpu().numpy(), x_h) and np.array_equal(d_w.cpu().numpy(), w_h)
     assert np.all(st_h == 0) and np.array_equal(d_st.cpu().numpy(), st_h)
+
+
+def test_reference_ho_qp_test_program():
+    """The reference's ho_qp_test.cpp checks, in C++, against legged::HoQp on the GPU (tests/cpp/ho_qp_test.cpp)."""
+    import subprocess
+
+    from legged_mpc_control_amd import build as B
+
+    exe = B.build_cpp_hoqp_test()
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ho_qp_test OK"), out.stdout + out.stderr
