@@ -43,6 +43,7 @@ extern "C" {
 #define LMPC_HOQP_MAX_VARS 64
 #define LMPC_HOQP_MAX_ROWS 64      /* equality or inequality rows of one level */
 #define LMPC_HOQP_MAX_STACKED 128  /* frozen + own inequality rows at any level */
+#define LMPC_HOQP_MAX_LDS_BYTES 65536 /* one chain's LDS block (lmpc_hoqp_lds_bytes) must fit one workgroup */
 
 typedef struct {
     int32_t num_vars;                          /* n (wbc.h:18: 18 + 12 + 12 = 42 for the WBC) */
@@ -63,8 +64,12 @@ typedef struct lmpc_hoqp_ctx lmpc_hoqp_ctx;
  * n = 42, levels (30 eq, 44 ineq), (18 eq), (12 eq). */
 void lmpc_hoqp_dims_wbc(lmpc_hoqp_dims* d);
 void lmpc_hoqp_options_default(lmpc_hoqp_options* o);
-/* doubles per instance record; < 0 (LMPC_ERR_ARG) if the dimensions are outside the limits above */
+/* doubles per instance record; < 0 (LMPC_ERR_ARG) if the dimensions are outside the limits above, including
+ * an LDS block over LMPC_HOQP_MAX_LDS_BYTES */
 int64_t lmpc_hoqp_record_len(const lmpc_hoqp_dims* d);
+/* LDS bytes one chain occupies: (max stacked rows + max(np, max eq rows)) * (np + 1) doubles + vectors, np = n
+ * rounded up to 16 (the WBC: 40 448 B, four chains per CU); sets how many chains share a CU */
+int64_t lmpc_hoqp_lds_bytes(const lmpc_hoqp_dims* d);
 int lmpc_hoqp_slack_len(const lmpc_hoqp_dims* d); /* total inequality rows */
 
 int lmpc_hoqp_create(const lmpc_hoqp_dims* d, int max_batch, int device, lmpc_hoqp_ctx** out);

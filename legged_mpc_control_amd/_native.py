@@ -40,7 +40,7 @@ ABI_VERSION = 4
 # include/lmpc/lmpc_hoqp.h: batched hierarchical QP (whole-body control)
 HOQP_SYMBOLS = (
     "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
-    "lmpc_hoqp_create", "lmpc_hoqp_destroy", "lmpc_hoqp_set_options", "lmpc_hoqp_solve_batch",
+    "lmpc_hoqp_lds_bytes", "lmpc_hoqp_create", "lmpc_hoqp_destroy", "lmpc_hoqp_set_options", "lmpc_hoqp_solve_batch",
     "lmpc_hoqp_solve_device", "lmpc_hoqp_sync", "lmpc_wbc_tasks", "lmpc_wbc_tasks_device",
 )
 HOQP_MAX_LEVELS = 4
@@ -241,6 +241,8 @@ def lib():
         L.lmpc_hoqp_options_default.restype = None
         L.lmpc_hoqp_record_len.argtypes = [hdp]
         L.lmpc_hoqp_record_len.restype = ctypes.c_int64
+        L.lmpc_hoqp_lds_bytes.argtypes = [hdp]
+        L.lmpc_hoqp_lds_bytes.restype = ctypes.c_int64
         L.lmpc_hoqp_slack_len.argtypes = [hdp]
         L.lmpc_hoqp_slack_len.restype = ctypes.c_int
         L.lmpc_hoqp_create.argtypes = [hdp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]

@@ -50,6 +50,8 @@ struct DeviceScope {
     DeviceScope& operator=(const DeviceScope&) = delete;
 };
 
+void fill_dev(lmpc::HoqpDev& P, const lmpc_hoqp_dims* d);
+
 bool dims_ok(const lmpc_hoqp_dims* d) {
     if (!d || d->num_vars < 1 || d->num_vars > LMPC_HOQP_MAX_VARS || d->num_levels < 1 ||
         d->num_levels > LMPC_HOQP_MAX_LEVELS)
@@ -62,7 +64,9 @@ bool dims_ok(const lmpc_hoqp_dims* d) {
         stacked += d->ineq_rows[l];
         if (stacked > LMPC_HOQP_MAX_STACKED) return false;
     }
-    return true;
+    lmpc::HoqpDev P;  // one chain's LDS block (constraint rows + K, lmpc_hoqp.hip) must fit one workgroup
+    fill_dev(P, d);
+    return lmpc::hq_lds_doubles(P) * sizeof(double) <= (size_t)LMPC_HOQP_MAX_LDS_BYTES;
 }
 
 void fill_dev(lmpc::HoqpDev& P, const lmpc_hoqp_dims* d) {
@@ -150,6 +154,15 @@ void lmpc_hoqp_options_default(lmpc_hoqp_options* o) {
     o->tol_res = 1e-7;
 }
 
+int64_t lmpc_hoqp_lds_bytes(const lmpc_hoqp_dims* d) {
+    if (!d || d->num_vars < 1 || d->num_vars > LMPC_HOQP_MAX_VARS || d->num_levels < 1 ||
+        d->num_levels > LMPC_HOQP_MAX_LEVELS)
+        return LMPC_ERR_ARG;
+    lmpc::HoqpDev P;
+    fill_dev(P, d);
+    return (int64_t)(lmpc::hq_lds_doubles(P) * sizeof(double));
+}
+
 int64_t lmpc_hoqp_record_len(const lmpc_hoqp_dims* d) {
     if (!dims_ok(d)) return LMPC_ERR_ARG;
     int64_t len = 0;
@@ -184,9 +197,6 @@ int lmpc_hoqp_create(const lmpc_hoqp_dims* d, int max_batch, int device, lmpc_ho
               hipMalloc(&c->d_out, outd * sizeof(double)) == hipSuccess &&
               hipMalloc(&c->d_st, (size_t)max_batch * (1 + c->P.L) * sizeof(int32_t)) == hipSuccess &&
               ensure_scratch(c, max_batch) == hipSuccess;
-    // the kernel's LDS block must fit one workgroup
-    const size_t lds = lmpc::hq_lds_doubles(c->P) * sizeof(double);
-    ok = ok && lds <= 64 * 1024;
     if (!ok) {
         lmpc_hoqp_destroy(c);
         return LMPC_ERR_ALLOC;

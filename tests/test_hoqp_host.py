@@ -56,6 +56,13 @@ def test_dims_record_layout_and_limits():
     bad.num_levels = 3
     bad.ineq_rows[0] = bad.ineq_rows[1] = bad.ineq_rows[2] = 60  # 180 stacked rows > 128
     assert lib.lmpc_hoqp_record_len(ctypes.byref(bad)) == -1
+    assert lib.lmpc_hoqp_lds_bytes(ctypes.byref(d)) == 40448  # the WBC: four chains per CU
+    big = N.LmpcHoqpDims()  # 64 variables with 128 stacked rows: 107 KB of LDS, over one workgroup's 64 KB
+    big.num_vars, big.num_levels = 64, 2
+    big.eq_rows[0] = big.eq_rows[1] = 64
+    big.ineq_rows[0] = big.ineq_rows[1] = 64
+    assert lib.lmpc_hoqp_lds_bytes(ctypes.byref(big)) > 65536
+    assert lib.lmpc_hoqp_record_len(ctypes.byref(big)) == -1
     o = N.LmpcHoqpOptions()
     lib.lmpc_hoqp_options_default(ctypes.byref(o))
     assert o.max_iter == 60 and o.tol_mu == 1e-13 and o.tol_res == 1e-7
