@@ -1,9 +1,10 @@
 #!/bin/bash
 # Dev tool (GPU box): A/B kernel times of diagnostic library builds over the bench configs.
 #   tools/ab_bench.sh TAG [TAG ...]   (libraries tools/build/liblmpc_TAG.so, built beforehand)
+#   AB_SPECS="2:50 4:3" picks configs:steps (suffix gi / off on the config: that dense path)
 for tag in "$@"; do
-  for spec in ${AB_SPECS:-"2 20" "2gi 20" "2off 20" "3 5" "4 3" "5 5"}; do
-    set -- $spec
+  for spec in ${AB_SPECS:-2:20 2gi:20 2off:20 3:5 4:3 5:5}; do
+    set -- ${spec/:/ }
     cfg=${1%gi}; cfg=${cfg%off}; steps=$2
     env=""
     case "$1" in *gi) env="LMPC_DENSE=gi";; *off) env="LMPC_DENSE=0";; esac
