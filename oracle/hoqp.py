@@ -179,7 +179,22 @@ def solve_ext(K, rhs):
 
 def qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
     """Primal active-set method (Nocedal & Wright, Alg. 16.3).  Returns (x, mu, info); mu >= 0 are
-    the multipliers of D x <= f (H x + c + D'mu = 0 at the optimum)."""
+    the multipliers of D x <= f (H x + c + D'mu = 0 at the optimum).  A degenerate vertex (more rows
+    active than it has dimensions, e.g. a friction pyramid at its apex projected on a small null space)
+    can make the method cycle; it is then re-run on bounds perturbed by 1e-13 of their scale, row by
+    row (Charnes' anti-cycling perturbation), which moves the optimum by that much."""
+    try:
+        return _qp_active_set(H, c, D, f, x0, max_iter, tol)
+    except RuntimeError:
+        m = D.shape[0]
+        eps = 1e-13 * (1.0 + float(np.max(np.abs(f)))) if m else 0.0
+        fp = f + eps * (1.0 + np.arange(m)) / max(m, 1)
+        x, mu, info = _qp_active_set(H, c, D, fp, x0, max_iter, tol)
+        info["perturbed"] = eps
+        return x, mu, info
+
+
+def _qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
     n, m = H.shape[0], D.shape[0]
     x = np.array(x0, dtype=np.longdouble)
     scale = 1.0 + np.max(np.abs(f)) if m else 1.0
@@ -195,6 +210,7 @@ def qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
             Wi.append(i)
     W = Wi
     at_min = False
+    seen, bland = set(), False  # anti-cycling: a working set seen twice at a stationary point -> Bland's rule
     for it in range(max_iter):
         g = np.asarray(H, dtype=np.longdouble) @ x + c
         k = len(W)
@@ -214,7 +230,14 @@ def qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
                 mu = np.zeros(m)
                 mu[W] = lam
                 return x.astype(np.float64), mu, dict(iters=it, working_set=list(W))
-            W.pop(int(np.argmin(lam)))
+            key = frozenset(W)
+            bland = bland or key in seen
+            seen.add(key)
+            if bland:  # drop the lowest-index row with a negative multiplier (degenerate vertices cycle otherwise)
+                neg = [j for j in range(k) if lam[j] < -1e-14 * (1.0 + np.max(np.abs(lam)))]
+                W.pop(min(neg, key=lambda j: W[j]))
+            else:
+                W.pop(int(np.argmin(lam)))
             continue
         alpha, block = 1.0, -1
         pn = float(np.max(np.abs(p)))
@@ -226,7 +249,9 @@ def qp_active_set(H, c, D, f, x0, max_iter=500, tol=1e-12):
             # (e.g. a zero inequality row's slack bound 0 - w <= 0 duplicates -w <= 0)
             if dp > 1e-13 * pn * float(np.max(np.abs(D[i]))):
                 a = float((f[i] - D[i] @ x)) / dp
-                if a < alpha:
+                # a row in the span of the working set cannot block a direction in its null space: it only
+                # does so by rounding (degenerate vertices, e.g. a pyramid at its apex)
+                if a < alpha and np.linalg.matrix_rank(D[W + [i]]) == k + 1:
                     alpha, block = a, i
         x = x + np.longdouble(max(alpha, 0.0)) * p
         if block >= 0:
