@@ -123,6 +123,10 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
         if (mu <= tol * scale and res <= rtol * scale) or (mu <= float(os.environ.get('STALL_MU', 1e-16)) * scale and res <= 1e3 * rtol * scale):
             break
         w1, w2, w3 = z1 / s1, z2 / s2, z3 / s3
+        wcap = float(os.environ.get("WCAP", 0))
+        if wcap:  # bounded weights: rows whose z/s passes the cap are held by a fixed penalty
+            cap = wcap * max(1.0, float(np.max(np.diag(Hy))))
+            w1, w2, w3 = np.minimum(w1, cap), np.minimum(w2, cap), np.minimum(w3, cap)
         dlt = 1.0 + w1 + w3
         w3h = w3 * (1.0 + w1) / dlt
         K = Hy + (P.T @ (w2[:, None] * P) if p else 0) + (Dz.T @ (w3h[:, None] * Dz) if s else 0)
