@@ -36,6 +36,7 @@ constexpr double HQ_REG = 1e-12;        // HoQp.cpp:84
 constexpr double HQ_PIV_FLOOR = 1e-13;  // relative to max(1, largest diagonal entry of K)
 constexpr double HQ_PIV_BIG = 1e64;     // pivot of a frozen coordinate
 constexpr double HQ_FRAC = 0.99;        // fraction of the step to the boundary
+constexpr double HQ_DIRECT_TOL = 1e-12; // frozen-row excess (x scale) an unconstrained minimiser may keep
 
 typedef __attribute__((address_space(3))) int lint;
 
@@ -178,10 +179,12 @@ __device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, 
 }
 
 // Lower tiles (I >= J) of sum_r w_r M[r][.]' M[r][.] over rows 0..rows-1 of an LDS matrix (stride ld,
-// np columns), accumulated onto acc[tile(I,J)] (w == nullptr: unit weights).
+// columns 0..16 nt - 1), accumulated onto acc[tile(I,J)] (w == nullptr: unit weights).
 __device__ __forceinline__ int tid(int I, int J) { return I * (I + 1) / 2 + J; }
-__device__ __forceinline__ void sym_tiles(const HoqpDev& P, const ldouble* M, int ld, int rows, const ldouble* w, d4 acc[10],
-                          int lane) {
+// 16-wide tiles that cover the level's nd coordinates (at least one): columns nd..np-1 of G, R and Z are zero
+__device__ __forceinline__ int nd_tiles(int nd) { return nd > 16 ? (nd + 15) >> 4 : 1; }
+__device__ __forceinline__ void sym_tiles(const ldouble* M, int ld, int rows, const ldouble* w, int nt, d4 acc[10],
+                                          int lane) {
     const int kq = lane >> 4, mm = lane & 15;
     for (int r0 = 0; r0 < rows; r0 += 4) {
         const int r = r0 + kq;
@@ -189,10 +192,10 @@ __device__ __forceinline__ void sym_tiles(const HoqpDev& P, const ldouble* M, in
         const double wr = live ? (w ? w[r] : 1.0) : 0.0;
         double v[4];
 #pragma unroll
-        for (int I = 0; I < 4; ++I) v[I] = (live && I < P.nt) ? M[r * ld + 16 * I + mm] : 0.0;
+        for (int I = 0; I < 4; ++I) v[I] = (live && I < nt) ? M[r * ld + 16 * I + mm] : 0.0;
 #pragma unroll
         for (int I = 0; I < 4; ++I)
-            if (I < P.nt) {
+            if (I < nt) {
                 const double a = wr * v[I];
 #pragma unroll
                 for (int J = 0; J <= I; ++J) acc[tid(I, J)] = MFMA64(a, v[J], acc[tid(I, J)]);
@@ -200,15 +203,31 @@ __device__ __forceinline__ void sym_tiles(const HoqpDev& P, const ldouble* M, in
     }
 }
 
-// Cholesky factor of K (nd x nd, lower) with a pivot floor, lane i = row i held in registers (kr[j] = K_ij,
-// statically indexed: NP = np unrolls every loop); column k is broadcast through LDS (S.dy as the buffer) and
-// applied to every row at once.  The factor goes back to S.KL (lower part), dI[k] = 1 / L_kk.
+// LDL' factor of K (nd x nd) with a pivot floor, lane i = row i held in registers (kr[j] = K_ij, statically
+// indexed: NP = np unrolls every loop).  Step k broadcasts the raw column K_jk (rows j > k) through LDS (S.dy
+// as the buffer) before its pivot is known, so the LDS round trip overlaps the pivot's reciprocal chain; row
+// i's multiplier K_ik / d_k is lane-local.  Row updates stop at the last 16-wide block that holds live
+// columns.  The unit lower factor goes back to S.KL (lower part), dI[k] = 1 / d_k.
 template <int NP>
-__device__ __attribute__((noinline)) void chol_floor(const HS& S, int ls, int nd, int lane) {
+__device__ __attribute__((noinline)) void chol_floor(const HS& S_, int ls, int nd, int lane) {
+    // local copies: members read through a reference (a flat pointer, which may alias LDS) would be
+    // reloaded after every LDS store
+    const HS S = S_;
+    nd = __builtin_amdgcn_readfirstlane(nd);  // arguments arrive in VGPRs: scalar branches, not exec masks
+    ls = __builtin_amdgcn_readfirstlane(ls);
     double kr[NP];
     const bool live = lane < nd;
+    const int nt = nd_tiles(nd);
 #pragma unroll
-    for (int j = 0; j < NP; ++j) kr[j] = (live && j < nd) ? S.KL[lane * ls + j] : 0.0;
+    for (int j = 0; j < NP; ++j) kr[j] = 0.0;
+    if (live) {  // one exec region, loads unmasked: columns nd..16 nt - 1 of K are zero (zero columns of Z)
+#pragma unroll
+        for (int J = 0; J < NP / 16; ++J)
+            if (J < nt) {
+#pragma unroll
+                for (int j = 16 * J; j < 16 * J + 16; ++j) kr[j] = S.KL[lane * ls + j];
+            }
+    }
     const double dmax = wave_max(live ? S.KL[lane * ls + lane] : 0.0);
     const double thr = HQ_PIV_FLOOR * fmax(1.0, dmax);
     ldouble* col = S.dy;
@@ -216,74 +235,100 @@ __device__ __attribute__((noinline)) void chol_floor(const HS& S, int ls, int nd
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         if (k < nd) {
+            if (lane < NP) col[lane] = lane > k ? kr[k] : 0.0;  // col = S.dy has np = NP entries
+            LMPC_SYNC();
+            double cj[NP];  // the whole column loaded ahead of the pivot chain (dead rows hold zeros)
+#pragma unroll
+            for (int j = k + 1; j < NP; ++j) cj[j] = col[j];
             const double pkk = readlane_f64(kr[k], k);
             const double piv = pkk > thr ? pkk : HQ_PIV_BIG;
-            double inv = rsq_nr(piv);
-            inv = inv * fma(-0.5 * piv * inv, inv, 1.5);  // second Newton step: 1/sqrt to rounding
-            const double l = kr[k] * inv;  // L_ik on rows i > k
-            kr[k] = lane == k ? piv * inv : l;
+            const double inv = rcp_nr(piv);
+            const double l = kr[k] * inv;
             di = lane == k ? inv : di;
-            if (lane < NP) col[lane] = lane > k ? l : 0.0;  // col = S.dy has np = NP entries
-            LMPC_SYNC();
 #pragma unroll
-            for (int j = k + 1; j < NP; ++j) kr[j] = fma(-l, col[j], kr[j]);  // rows <= k: upper part, unused
+            for (int J = k / 16; J < NP / 16; ++J)
+                if (J == 0 || J < nt) {  // nt >= 1: block 0 unconditional
+#pragma unroll
+                    for (int j = (16 * J > k + 1 ? 16 * J : k + 1); j < 16 * J + 16; ++j) kr[j] = fma(-l, cj[j], kr[j]);
+                }
             LMPC_SYNC();
         }
     }
-    // store the unit lower factor Lt = L diag(1/L_kk) (K = Lt D^2 Lt', D = diag(L_kk)): its substitutions need
-    // no division per step
+    // store the unit lower factor Lt (K = Lt D Lt'; its substitutions need no division per step) over the live
+    // tiles with its diagonal, upper part and dead rows zeroed, so the solves load it without masks
     if (live) S.dI[lane] = di;
     LMPC_SYNC();
+    if (lane < NP) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j)
-        if (live && j < lane) S.KL[lane * ls + j] = kr[j] * S.dI[j];
+        for (int J = 0; J < NP / 16; ++J)
+            if (J < nt) {
+#pragma unroll
+                for (int j = 16 * J; j < 16 * J + 16; ++j) {
+                    const double dj = S.dI[j];  // unconditional broadcast load, then a select
+                    S.KL[lane * ls + j] = (live && j < lane) ? kr[j] * dj : 0.0;
+                }
+            }
+    }
     LMPC_SYNC();
 }
 
-// K u = rhs with K = Lt D^2 Lt' (Lt unit lower in S.KL, D^-1 in S.dI): rhs in lane i (i < nd); returns u in
-// lane i, also stored to out[i].  Lt v = rhs, then Lt' u = D^-2 v.  The row and then the column of Lt a lane
-// needs are loaded up front (NP statically indexed registers); a step of either substitution is one readlane
-// broadcast and one fma, in blocks of 8 steps guarded by nd.
+// K u = rhs with K = Lt D Lt' (Lt unit lower in S.KL, zero elsewhere over the live tiles; D^-1 in S.dI): rhs in
+// lane i (i < nd); returns u in lane i, also stored to out[i].  Lt v = rhs, then Lt' u = D^-1 v.  The row and
+// then the column of Lt a lane needs are loaded up front (NP statically indexed registers); a step of either
+// substitution is one readlane broadcast and one fma, in blocks of 8 steps guarded by nd.  A lane's own entry
+// needs no select: its coefficients from its own step on are zero, so its accumulator stops at its solution.
 template <int NP>
-__device__ __attribute__((noinline)) double chol_solve(const HS& S, int ls, int nd, double rhs, ldouble* out,
+__device__ __attribute__((noinline)) double chol_solve(const HS& S_, int ls, int nd, double rhs, ldouble* out,
                                                        int lane) {
+    const HS S = S_;
+    nd = __builtin_amdgcn_readfirstlane(nd);
+    ls = __builtin_amdgcn_readfirstlane(ls);
     const bool live = lane < nd;
-    const double di = live ? S.dI[lane] : 0.0;
+    const int nt = nd_tiles(nd);
     double lr[NP];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) lr[k] = (live && k < lane) ? S.KL[lane * ls + k] : 0.0;  // row lane of Lt
-    double acc = live ? rhs : 0.0, v = 0.0;
+    for (int k = 0; k < NP; ++k) lr[k] = 0.0;
+    double di = 0.0;
+    if (live) {  // row lane of Lt
+        di = S.dI[lane];
+#pragma unroll
+        for (int J = 0; J < NP / 16; ++J)
+            if (J < nt) {
+#pragma unroll
+                for (int k = 16 * J; k < 16 * J + 16; ++k) lr[k] = S.KL[lane * ls + k];
+            }
+    }
+    double acc = live ? rhs : 0.0;
 #pragma unroll
     for (int k0 = 0; k0 < NP; k0 += 8)
         if (k0 < nd) {
 #pragma unroll
-            for (int k = k0; k < k0 + 8; ++k) {  // Lt v = rhs
-                const double vk = readlane_f64(acc, k);
-                v = lane == k ? vk : v;
-                acc = fma(-lr[k], vk, acc);
-            }
+            for (int k = k0; k < k0 + 8; ++k) acc = fma(-lr[k], readlane_f64(acc, k), acc);  // Lt v = rhs
         }
+    if (live) {  // column lane of Lt
 #pragma unroll
-    for (int k = 0; k < NP; ++k) lr[k] = (live && k > lane && k < nd) ? S.KL[k * ls + lane] : 0.0;  // column
-    acc = v * di * di;
-    double sol = 0.0;
+        for (int J = 0; J < NP / 16; ++J)
+            if (J < nt) {
+#pragma unroll
+                for (int k = 16 * J; k < 16 * J + 16; ++k) lr[k] = S.KL[k * ls + lane];
+            }
+    }
+    acc *= di;
 #pragma unroll
     for (int k1 = NP; k1 > 0; k1 -= 8)
         if (k1 - 8 < nd) {
 #pragma unroll
-            for (int k = k1 - 1; k >= k1 - 8; --k) {  // Lt' u = D^-2 v
-                const double xk = readlane_f64(acc, k);
-                sol = lane == k ? xk : sol;
-                acc = fma(-lr[k], xk, acc);
-            }
+            for (int k = k1 - 1; k >= k1 - 8; --k) acc = fma(-lr[k], readlane_f64(acc, k), acc);  // Lt' u = D^-1 v
         }
-    if (live) out[lane] = sol;
+    if (live) out[lane] = acc;
     LMPC_SYNC();
-    return sol;
+    return acc;
 }
 
 // t = R_r . vec (row r, nd columns); loads issued eight at a time ahead of their fmas
-__device__ __attribute__((noinline)) double row_dot(const HS& S, int ls, int nd, int r, const ldouble* vec) {
+__device__ __attribute__((noinline)) double row_dot(const HS& S_, int ls, int nd, int r, const ldouble* vec) {
+    const HS S = S_;
+    nd = __builtin_amdgcn_readfirstlane(nd);
     double a0 = 0.0, a1 = 0.0;
     int j = 0;
     for (; j + 8 <= nd; j += 8) {
@@ -303,7 +348,9 @@ __device__ __attribute__((noinline)) double row_dot(const HS& S, int ls, int nd,
     return a0 + a1;
 }
 // (R' q)_j for lane j
-__device__ __attribute__((noinline)) double rt_dot(const HS& S, int ls, int nr, const ldouble* q, int lane) {
+__device__ __attribute__((noinline)) double rt_dot(const HS& S_, int ls, int nr, const ldouble* q, int lane) {
+    const HS S = S_;
+    nr = __builtin_amdgcn_readfirstlane(nr);
     double a0 = 0.0, a1 = 0.0;
     int r = 0;
     for (; r + 8 <= nr; r += 8) {
@@ -323,32 +370,33 @@ __device__ __attribute__((noinline)) double rt_dot(const HS& S, int ls, int nr, 
     return a0 + a1;
 }
 // (Hy y)_j for lane j < nd (Hy in global scratch, np x np)
-__device__ __attribute__((noinline)) double hy_dot(const HoqpDev& P, const gdouble* Hg, const ldouble* y, int nd,
+// every live 16-row block loaded in one batch (one global round trip); rows nd..16 nt - 1 of Hg and y are
+// zero, so the block-wide sum is exact
+template <int NP>
+__device__ __attribute__((noinline)) double hy_dot(const HoqpDev& P_, const gdouble* Hg, const ldouble* y, int nd,
                                                    int lane) {
+    const HoqpDev P = P_;
+    const int nt = nd_tiles(__builtin_amdgcn_readfirstlane(nd));
+    double hv[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) hv[i] = (i < 16 * nt) ? Hg[(int64_t)i * NP + lane] : 0.0;
     double a0 = 0.0, a1 = 0.0;
-    int i = 0;
-    for (; i + 8 <= nd; i += 8) {
-        double hv[8], yv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            hv[u] = Hg[(int64_t)(i + u) * P.np + lane];
-            yv[u] = y[i + u];
+    for (int i = 0; i < NP; i += 2)
+        if (i < 16 * nt) {
+            a0 = fma(hv[i], y[i], a0);
+            a1 = fma(hv[i + 1], y[i + 1], a1);
         }
-#pragma unroll
-        for (int u = 0; u < 8; u += 2) {
-            a0 = fma(hv[u], yv[u], a0);
-            a1 = fma(hv[u + 1], yv[u + 1], a1);
-        }
-    }
-    for (; i < nd; ++i) a0 = fma(Hg[(int64_t)i * P.np + lane], y[i], a0);
     return a0 + a1;
 }
 
 // Eigen FullPivLU of G (m x nd in S.KL) and Z' = Z ker(G) into Zn (n x np); returns the new nd.
 // Restates Eigen/src/LU/FullPivLU.h (3.3): compute() and kernel_retval::evalTo (tests/test_hoqp_oracle.py
 // pins the CPU restatement, oracle/hoqp.py fullpivlu / fullpivlu_kernel, that this follows step by step).
-__device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P, const HS& S, int m, int nd, const gdouble* Z, gdouble* Zn,
+__device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P_, const HS& S_, int m, int nd, const gdouble* Z, gdouble* Zn,
                                 int lane) {
+    const HS S = S_;
+    const HoqpDev P = P_;
     const int ls = hq_ls(P);
     const int size = m < nd ? m : nd;
     int nonzero = size;
@@ -534,11 +582,14 @@ __device__ __forceinline__ double gdot(const double* g, const ldouble* x, int n,
     return a0 + a1;
 }
 
-// Level setup: G = A Z (into S.KL), c = G'(A x - b) (S.c), Hy = G'G + 1e-12 I (Hg, full symmetric np x np).
+// Level setup: G = A Z (into S.KL), c = G'(A x - b) (S.c), Hy = G'G + 1e-12 I (Hg, full symmetric, the
+// 16-wide tiles that cover nd; row stride np).
 template <int NP>
-__device__ __attribute__((noinline)) void level_setup(const HoqpDev& P, const HS& S, const double* rec, int l,
+__device__ __attribute__((noinline)) void level_setup(const HoqpDev& P_, const HS& S_, const double* rec, int l,
                                                       int nd, const gdouble* Z, gdouble* Hg, int lane) {
-    const int ls = hq_ls(P), m = P.m[l];
+    const HS S = S_;
+    const HoqpDev P = P_;
+    const int ls = hq_ls(P), m = P.m[l], nt = nd_tiles(nd);
     if (lane < P.np) S.c[lane] = 0.0;
     d4 acc[10];
 #pragma unroll
@@ -556,14 +607,14 @@ __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P, const HS
             for (int i = 0; i < m; ++i) a = fma(S.KL[i * ls + lane], S.vb[i], a);
             S.c[lane] = a;
         }
-        sym_tiles(P, S.KL, ls, m, nullptr, acc, lane);
+        sym_tiles(S.KL, ls, m, nullptr, nt, acc, lane);
     }
     const int g = lane >> 4, cc = lane & 15;
 #pragma unroll
     for (int I = 0; I < 4; ++I)
 #pragma unroll
         for (int J = 0; J <= I; ++J)
-            if (I < P.nt) {
+            if (I < nt) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int row = 16 * I + 4 * i + g, col = 16 * J + cc;
@@ -575,26 +626,29 @@ __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P, const HS
             }
 }
 
-// K = Hy + R' diag(wh) R on the matrix cores (lower tiles) into S.KL.
-__device__ __attribute__((noinline)) void form_K(const HoqpDev& P, const HS& S, int nr, const gdouble* Hg, int lane) {
-    const int ls = hq_ls(P), g = lane >> 4, cc = lane & 15;
+// K = Hy + R' diag(wh) R on the matrix cores (lower tiles covering nd) into S.KL.
+__device__ __attribute__((noinline)) void form_K(const HoqpDev& P_, const HS& S_, int nr, int nd, const gdouble* Hg,
+                                                 int lane) {
+    const HS S = S_;
+    const HoqpDev P = P_;
+    const int ls = hq_ls(P), g = lane >> 4, cc = lane & 15, nt = nd_tiles(nd);
     d4 acc[10];
 #pragma unroll
     for (int I = 0; I < 4; ++I)
 #pragma unroll
         for (int J = 0; J <= I; ++J) {
             acc[tid(I, J)] = d4{0.0, 0.0, 0.0, 0.0};
-            if (I < P.nt) {
+            if (I < nt) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[tid(I, J)][i] = Hg[(int64_t)(16 * I + 4 * i + g) * P.np + 16 * J + cc];
             }
         }
-    sym_tiles(P, S.R, ls, nr, S.wh, acc, lane);
+    sym_tiles(S.R, ls, nr, S.wh, nt, acc, lane);
 #pragma unroll
     for (int I = 0; I < 4; ++I)
 #pragma unroll
         for (int J = 0; J <= I; ++J)
-            if (I < P.nt) {
+            if (I < nt) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) S.KL[(16 * I + 4 * i + g) * ls + 16 * J + cc] = acc[tid(I, J)][i];
             }
@@ -603,8 +657,10 @@ __device__ __attribute__((noinline)) void form_K(const HoqpDev& P, const HS& S, 
 
 // Constraint rows R = [D_stack; D_l] Z (rows 0..nr-1 of S.R).
 template <int NP>
-__device__ __attribute__((noinline)) void build_rows(const HoqpDev& P, const HS& S, const double* rec, int l, int p,
+__device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS& S_, const double* rec, int l, int p,
                                                      int nr, const gdouble* Z, int lane) {
+    const HS S = S_;
+    const HoqpDev P = P_;
     gemm_xz<NP>(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
 }
 
@@ -705,11 +761,31 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         const double scale = 1.0 + fmax(wave_max(lane < nd ? fabs(S.c[lane]) : 0.0), wave_max(bmax));
         const double mc = (double)(p + 2 * s);
         HSTAMP(2);
+        // ---- a level without inequalities of its own: its unconstrained minimiser y0 = -Hy^-1 c is the optimum
+        // whenever it satisfies every frozen row (KKT with zero multipliers), which one factorisation decides;
+        // a frozen row above its bound sends the level to the interior point from y = 0
+        bool direct = false;
+        if (s == 0) {
+            form_K(P, S, 0, nd, Hg, lane);
+            chol_floor<NP>(S, ls, nd, lane);
+            chol_solve<NP>(S, ls, nd, lane < nd ? -S.c[lane] : 0.0, S.y, lane);
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                if (r < nr) ok = ok && row_dot(S, ls, nd, r, S.y) <= W.bd[k] + HQ_DIRECT_TOL * scale;
+            }
+            ok = ok && (lane >= nd || isfinite((double)S.y[lane]));
+            direct = __ballot(!ok) == 0;
+            if (!direct && lane < P.np) S.y[lane] = 0.0;
+            LMPC_SYNC();
+        }
         // ---- interior point --------------------------------------------------------------------------
         int it = 0;
         bool numstop = false;  // left on a non-finite Newton direction
         double mu_last = 0.0;
         for (;; ++it) {
+            if (direct) break;
             // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
             double rp1[2], rpg[2], rdv[2];
             double cs = 0.0, res = 0.0;
@@ -736,7 +812,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             double rdy = 0.0;
             if (lane < nd) {
                 double a = S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
-                a += hy_dot(P, Hg, S.y, nd, lane);
+                a += hy_dot<NP>(P, Hg, S.y, nd, lane);
                 rdy = a;
                 res = fmax(res, fabs(a));
             }
@@ -764,7 +840,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 if (r < P.rmax) S.wh[r] = r >= nr ? 0.0 : (r < p ? wg[k] : wg[k] * (1.0 + w1[k]) * idl[k]);
             }
             LMPC_SYNC();
-            form_K(P, S, nr, Hg, lane);
+            form_K(P, S, nr, nd, Hg, lane);
             HSTAMP(4);
             chol_floor<NP>(S, ls, nd, lane);
             HSTAMP(5);
