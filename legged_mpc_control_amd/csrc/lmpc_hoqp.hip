@@ -14,13 +14,13 @@
 //   solve   min 1/2 y'Hy y + c'y + 1/2 |v|^2  s.t. -v <= 0, D_stack Z y <= h, D_l Z y - v <= g   (:158-174)
 //           by a Mehrotra interior point over (y, v) with v eliminated: per iteration
 //           K = Hy + R' diag(w) R (w = z/s on frozen rows, w3 (1 + w1)/(1 + w1 + w3) on own rows) on the
-//           matrix cores, its Cholesky factor with a pivot floor (Hy is singular in double along ker G,
+//           matrix cores, its LDL' factor with a pivot floor (Hy is singular in double along ker G,
 //           where 1e-12 is below the rounding of G'G: such a pivot freezes its coordinate), two solves;
 //           afterwards v = max(0, D_l Z y - g) exactly for the final y
 //   output  x += Z y (HoQp.h:41-45), w_l = v, and Z <- Z'.
 // Layout: the instance records stay in HBM and are read by the level setup only; the level's constraint
 // rows R and K live in LDS (one wave = one instance, ~40 KB at the WBC's n = 42); Z, Z' and Hy live in a
-// per-instance global scratch (L2-resident), read once per level or once per iteration.
+// per-instance global scratch, read once per level or once per iteration.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -36,7 +36,6 @@ constexpr double HQ_REG = 1e-12;        // HoQp.cpp:84
 constexpr double HQ_PIV_FLOOR = 1e-13;  // relative to max(1, largest diagonal entry of K)
 constexpr double HQ_PIV_BIG = 1e64;     // pivot of a frozen coordinate
 constexpr double HQ_FRAC = 0.99;        // fraction of the step to the boundary
-constexpr double HQ_DIRECT_TOL = 1e-12; // frozen-row excess (x scale) an unconstrained minimiser may keep
 
 typedef __attribute__((address_space(3))) int lint;
 
@@ -178,6 +177,34 @@ __device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, 
     }
 }
 
+// Outlined helpers receive their arguments in VGPRs and their structs through flat pointers: counts are made
+// uniform again (scalar branches and loop bounds instead of exec masks), structs copied to locals once.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    return (int64_t)(((uint64_t)(uint32_t)uni((int)(u >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)u));
+}
+__device__ __forceinline__ HoqpDev uniform(const HoqpDev& p) {
+    HoqpDev q = p;
+    q.n = uni(p.n);
+    q.np = uni(p.np);
+    q.nt = uni(p.nt);
+    q.L = uni(p.L);
+#pragma unroll
+    for (int i = 0; i < HQ_MAX_LEVELS; ++i) {
+        q.m[i] = uni(p.m[i]);
+        q.s[i] = uni(p.s[i]);
+        q.off[i] = uni64(p.off[i]);
+    }
+    q.rec_len = uni64(p.rec_len);
+    q.slack_len = uni(p.slack_len);
+    q.rmax = uni(p.rmax);
+    q.kmax = uni(p.kmax);
+    q.max_iter = uni(p.max_iter);
+    q.scratch_len = uni64(p.scratch_len);
+    return q;
+}
+
 // Lower tiles (I >= J) of sum_r w_r M[r][.]' M[r][.] over rows 0..rows-1 of an LDS matrix (stride ld,
 // columns 0..16 nt - 1), accumulated onto acc[tile(I,J)] (w == nullptr: unit weights).
 __device__ __forceinline__ int tid(int I, int J) { return I * (I + 1) / 2 + J; }
@@ -210,11 +237,11 @@ __device__ __forceinline__ void sym_tiles(const ldouble* M, int ld, int rows, co
 // columns.  The unit lower factor goes back to S.KL (lower part), dI[k] = 1 / d_k.
 template <int NP>
 __device__ __attribute__((noinline)) void chol_floor(const HS& S_, int ls, int nd, int lane) {
-    // local copies: members read through a reference (a flat pointer, which may alias LDS) would be
-    // reloaded after every LDS store
+    // local copy: members read through the reference (a flat pointer, which may alias LDS) would be reloaded
+    // after every LDS store
     const HS S = S_;
-    nd = __builtin_amdgcn_readfirstlane(nd);  // arguments arrive in VGPRs: scalar branches, not exec masks
-    ls = __builtin_amdgcn_readfirstlane(ls);
+    nd = uni(nd);
+    ls = uni(ls);
     double kr[NP];
     const bool live = lane < nd;
     const int nt = nd_tiles(nd);
@@ -281,8 +308,8 @@ template <int NP>
 __device__ __attribute__((noinline)) double chol_solve(const HS& S_, int ls, int nd, double rhs, ldouble* out,
                                                        int lane) {
     const HS S = S_;
-    nd = __builtin_amdgcn_readfirstlane(nd);
-    ls = __builtin_amdgcn_readfirstlane(ls);
+    nd = uni(nd);
+    ls = uni(ls);
     const bool live = lane < nd;
     const int nt = nd_tiles(nd);
     double lr[NP];
@@ -328,7 +355,8 @@ __device__ __attribute__((noinline)) double chol_solve(const HS& S_, int ls, int
 // t = R_r . vec (row r, nd columns); loads issued eight at a time ahead of their fmas
 __device__ __attribute__((noinline)) double row_dot(const HS& S_, int ls, int nd, int r, const ldouble* vec) {
     const HS S = S_;
-    nd = __builtin_amdgcn_readfirstlane(nd);
+    nd = uni(nd);
+    ls = uni(ls);
     double a0 = 0.0, a1 = 0.0;
     int j = 0;
     for (; j + 8 <= nd; j += 8) {
@@ -350,7 +378,8 @@ __device__ __attribute__((noinline)) double row_dot(const HS& S_, int ls, int nd
 // (R' q)_j for lane j
 __device__ __attribute__((noinline)) double rt_dot(const HS& S_, int ls, int nr, const ldouble* q, int lane) {
     const HS S = S_;
-    nr = __builtin_amdgcn_readfirstlane(nr);
+    nr = uni(nr);
+    ls = uni(ls);
     double a0 = 0.0, a1 = 0.0;
     int r = 0;
     for (; r + 8 <= nr; r += 8) {
@@ -375,8 +404,8 @@ __device__ __attribute__((noinline)) double rt_dot(const HS& S_, int ls, int nr,
 template <int NP>
 __device__ __attribute__((noinline)) double hy_dot(const HoqpDev& P_, const gdouble* Hg, const ldouble* y, int nd,
                                                    int lane) {
-    const HoqpDev P = P_;
-    const int nt = nd_tiles(__builtin_amdgcn_readfirstlane(nd));
+    const HoqpDev P = uniform(P_);
+    const int nt = nd_tiles(uni(nd));
     double hv[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) hv[i] = (i < 16 * nt) ? Hg[(int64_t)i * NP + lane] : 0.0;
@@ -396,7 +425,9 @@ __device__ __attribute__((noinline)) double hy_dot(const HoqpDev& P_, const gdou
 __device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P_, const HS& S_, int m, int nd, const gdouble* Z, gdouble* Zn,
                                 int lane) {
     const HS S = S_;
-    const HoqpDev P = P_;
+    const HoqpDev P = uniform(P_);
+    m = uni(m);
+    nd = uni(nd);
     const int ls = hq_ls(P);
     const int size = m < nd ? m : nd;
     int nonzero = size;
@@ -588,7 +619,9 @@ template <int NP>
 __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P_, const HS& S_, const double* rec, int l,
                                                       int nd, const gdouble* Z, gdouble* Hg, int lane) {
     const HS S = S_;
-    const HoqpDev P = P_;
+    const HoqpDev P = uniform(P_);
+    l = uni(l);
+    nd = uni(nd);
     const int ls = hq_ls(P), m = P.m[l], nt = nd_tiles(nd);
     if (lane < P.np) S.c[lane] = 0.0;
     d4 acc[10];
@@ -630,7 +663,9 @@ __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P_, const H
 __device__ __attribute__((noinline)) void form_K(const HoqpDev& P_, const HS& S_, int nr, int nd, const gdouble* Hg,
                                                  int lane) {
     const HS S = S_;
-    const HoqpDev P = P_;
+    const HoqpDev P = uniform(P_);
+    nr = uni(nr);
+    nd = uni(nd);
     const int ls = hq_ls(P), g = lane >> 4, cc = lane & 15, nt = nd_tiles(nd);
     d4 acc[10];
 #pragma unroll
@@ -660,7 +695,10 @@ template <int NP>
 __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS& S_, const double* rec, int l, int p,
                                                      int nr, const gdouble* Z, int lane) {
     const HS S = S_;
-    const HoqpDev P = P_;
+    const HoqpDev P = uniform(P_);
+    l = uni(l);
+    p = uni(p);
+    nr = uni(nr);
     gemm_xz<NP>(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
 }
 
@@ -761,31 +799,11 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         const double scale = 1.0 + fmax(wave_max(lane < nd ? fabs(S.c[lane]) : 0.0), wave_max(bmax));
         const double mc = (double)(p + 2 * s);
         HSTAMP(2);
-        // ---- a level without inequalities of its own: its unconstrained minimiser y0 = -Hy^-1 c is the optimum
-        // whenever it satisfies every frozen row (KKT with zero multipliers), which one factorisation decides;
-        // a frozen row above its bound sends the level to the interior point from y = 0
-        bool direct = false;
-        if (s == 0) {
-            form_K(P, S, 0, nd, Hg, lane);
-            chol_floor<NP>(S, ls, nd, lane);
-            chol_solve<NP>(S, ls, nd, lane < nd ? -S.c[lane] : 0.0, S.y, lane);
-            bool ok = true;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int r = lane + 64 * k;
-                if (r < nr) ok = ok && row_dot(S, ls, nd, r, S.y) <= W.bd[k] + HQ_DIRECT_TOL * scale;
-            }
-            ok = ok && (lane >= nd || isfinite((double)S.y[lane]));
-            direct = __ballot(!ok) == 0;
-            if (!direct && lane < P.np) S.y[lane] = 0.0;
-            LMPC_SYNC();
-        }
         // ---- interior point --------------------------------------------------------------------------
         int it = 0;
         bool numstop = false;  // left on a non-finite Newton direction
         double mu_last = 0.0;
         for (;; ++it) {
-            if (direct) break;
             // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
             double rp1[2], rpg[2], rdv[2];
             double cs = 0.0, res = 0.0;
