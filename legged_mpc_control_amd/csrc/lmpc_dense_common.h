@@ -303,6 +303,7 @@ struct DiagInv {
 // Outlined (one call site): the elimination gets the caller-saved registers to itself instead of
 // competing with the factor tiles and the leg state that are live around it.
 static __device__ __attribute__((noinline)) DiagInv diag_inverse(ldouble* scr, d4 M, int amask, int lane) {
+    amask = __builtin_amdgcn_readfirstlane(amask);  // uniform (tile_mask), but arguments arrive in VGPRs
     ldouble* pv = scr;              // 96: pivot rows o..o+2 of T (48) then of W (48), 16 columns each
     ldouble* tr = scr + 96;         // 16 x 17: transpose staging of W
     ldouble* dummy = scr + 96 + 272;  // 112: sink of the stores of lanes that hold no pivot row

@@ -352,51 +352,57 @@ __device__ __attribute__((noinline)) double chol_solve(const HS& S_, int ls, int
     return acc;
 }
 
-// t = R_r . vec (row r, nd columns); loads issued eight at a time ahead of their fmas
+// t = R_r . vec (row r): 16-column blocks up to the level's live tiles, each block's 32 loads issued ahead of
+// its fmas (columns nd..16 nt - 1 of R and of vec are zero)
+template <int NP>
 __device__ __attribute__((noinline)) double row_dot(const HS& S_, int ls, int nd, int r, const ldouble* vec) {
     const HS S = S_;
-    nd = uni(nd);
     ls = uni(ls);
-    double a0 = 0.0, a1 = 0.0;
-    int j = 0;
-    for (; j + 8 <= nd; j += 8) {
-        double rv[8], vv[8];
+    const int nt = nd_tiles(uni(nd));
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            rv[u] = S.R[r * ls + j + u];
-            vv[u] = vec[j + u];
-        }
+    for (int J = 0; J < NP / 16; ++J)
+        if (J == 0 || J < nt) {
+            double rv[16], vv[16];
 #pragma unroll
-        for (int u = 0; u < 8; u += 2) {
-            a0 = fma(rv[u], vv[u], a0);
-            a1 = fma(rv[u + 1], vv[u + 1], a1);
+            for (int u = 0; u < 16; ++u) {
+                rv[u] = S.R[r * ls + 16 * J + u];
+                vv[u] = vec[16 * J + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) a[u & 3] = fma(rv[u], vv[u], a[u & 3]);
         }
-    }
-    for (; j < nd; ++j) a0 = fma(S.R[r * ls + j], vec[j], a0);
-    return a0 + a1;
+    return (a[0] + a[1]) + (a[2] + a[3]);
 }
-// (R' q)_j for lane j
+// (R' q)_j for lane j: 16-row blocks, each block's 32 loads issued ahead of its fmas; rows past nr are never
+// read (that LDS is not written at this level)
 __device__ __attribute__((noinline)) double rt_dot(const HS& S_, int ls, int nr, const ldouble* q, int lane) {
     const HS S = S_;
     nr = uni(nr);
     ls = uni(ls);
-    double a0 = 0.0, a1 = 0.0;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
     int r = 0;
-    for (; r + 8 <= nr; r += 8) {
-        double rv[8], qv[8];
+    for (; r + 16 <= nr; r += 16) {
+        double rv[16], qv[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 16; ++u) {
             rv[u] = S.R[(r + u) * ls + lane];
             qv[u] = q[r + u];
         }
 #pragma unroll
-        for (int u = 0; u < 8; u += 2) {
-            a0 = fma(rv[u], qv[u], a0);
-            a1 = fma(rv[u + 1], qv[u + 1], a1);
-        }
+        for (int u = 0; u < 16; ++u) a[u & 3] = fma(rv[u], qv[u], a[u & 3]);
     }
-    for (; r < nr; ++r) a0 = fma(S.R[r * ls + lane], q[r], a0);
-    return a0 + a1;
+    if (r < nr) {
+        double rv[16], qv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            rv[u] = r + u < nr ? S.R[(r + u) * ls + lane] : 0.0;
+            qv[u] = r + u < nr ? q[r + u] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) a[u & 3] = fma(rv[u], qv[u], a[u & 3]);
+    }
+    return (a[0] + a[1]) + (a[2] + a[3]);
 }
 // (Hy y)_j for lane j < nd (Hy in global scratch, np x np)
 // every live 16-row block loaded in one batch (one global round trip); rows nd..16 nt - 1 of Hg and y are
@@ -812,7 +818,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 const int r = lane + 64 * k;
                 rp1[k] = rpg[k] = rdv[k] = 0.0;
                 if (r < nr) {
-                    const double ty = row_dot(S, ls, nd, r, S.y);
+                    const double ty = row_dot<NP>(S, ls, nd, r, S.y);
                     S.q[r] = W.zg[k];
                     if (r < p) {
                         rpg[k] = ty + W.sg[k] - W.bd[k];
@@ -894,7 +900,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                     const int r = lane + 64 * k;
                     ds1[k] = dsg[k] = dz1[k] = dzg[k] = dv[k] = 0.0;
                     if (r < nr) {
-                        const double td = row_dot(S, ls, nd, r, S.dy);
+                        const double td = row_dot<NP>(S, ls, nd, r, S.dy);
                         double cg = td;
                         if (r >= p) {
                             dv[k] = (rv[k] + wg[k] * td) * idl[k];
@@ -983,7 +989,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int r = lane + 64 * k;
-            if (r >= p && r < nr) wo[r] = fmax(0.0, row_dot(S, ls, nd, r, S.y) - W.bd[k]);
+            if (r >= p && r < nr) wo[r] = fmax(0.0, row_dot<NP>(S, ls, nd, r, S.y) - W.bd[k]);
         }
         double xn = 0.0;
         if (lane < P.n) {
