@@ -77,7 +77,8 @@ void lmpc_hoqp_destroy(lmpc_hoqp_ctx* ctx);
 int lmpc_hoqp_set_options(lmpc_hoqp_ctx* ctx, const lmpc_hoqp_options* o);
 
 /* Host buffers, synchronous.  status [batch] (LMPC_QP_CONVERGED / LMPC_QP_MAX_ITER: some level stopped at
- * max_iter, best iterate kept / LMPC_QP_NAN: zeros returned) and iters [batch][num_levels] may be NULL. */
+ * max_iter, best iterate kept / LMPC_QP_NAN: a non-finite record entry, residual or result; zeros returned)
+ * and iters [batch][num_levels] may be NULL. */
 int lmpc_hoqp_solve_batch(lmpc_hoqp_ctx* ctx, const double* tasks, int batch, double* x, double* slack,
                           int32_t* status, int32_t* iters);
 /* Device buffers (resident in HBM), asynchronous on `stream` (hipStream_t; NULL = the null stream, as in

@@ -177,6 +177,10 @@ __device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, 
     }
 }
 
+// max that propagates NaN (fmax drops it): a non-finite input must reach the stop test
+__device__ __forceinline__ double nan_max(double a, double b) { return (a > b || a != a) ? a : b; }
+struct OpNanMax { __device__ static double f(double a, double b) { return nan_max(a, b); } };
+
 // Outlined helpers receive their arguments in VGPRs and their structs through flat pointers: counts are made
 // uniform again (scalar branches and loop bounds instead of exec masks), structs copied to locals once.
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -734,6 +738,10 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     gdouble* Hg = (gdouble*)(scratch + (int64_t)b * P.scratch_len + 2 * (int64_t)P.n * P.np);
     gdouble* wo = (gdouble*)(wout + (int64_t)b * P.slack_len);
     int zc = 0;
+    // a non-finite record entry reaches the first residuals of its level (the residual maximum propagates NaN);
+    // so does an overflow: zeros and LMPC_QP_NAN, as the MPC path returns zero forces for a NaN solve
+    // (ConvexQPSolver.cpp:321-326)
+    bool nonfin = false;
     // Z = I, x = 0
     if (lane < P.n)
         for (int j = 0; j < P.np; ++j) zbuf[0][(int64_t)lane * P.np + j] = (j == lane) ? 1.0 : 0.0;
@@ -829,7 +837,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                         rdv[k] = W.v[k] - W.z1[k] - W.zg[k];
                         cs += W.sg[k] * W.zg[k] + W.s1[k] * W.z1[k];
                     }
-                    res = fmax(res, fmax(fabs(rpg[k]), fmax(fabs(rp1[k]), fabs(rdv[k]))));
+                    res = nan_max(res, nan_max(fabs(rpg[k]), nan_max(fabs(rp1[k]), fabs(rdv[k]))));
                 }
             }
             LMPC_SYNC();
@@ -838,12 +846,16 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 double a = S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
                 a += hy_dot<NP>(P, Hg, S.y, nd, lane);
                 rdy = a;
-                res = fmax(res, fabs(a));
+                res = nan_max(res, fabs(a));
             }
             const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
             mu_last = mu;
-            res = wave_max(res);
+            res = wave_reduce<OpNanMax>(res);
             HSTAMP(3);
+            if (!(isfinite(mu) && isfinite(res))) {
+                nonfin = true;
+                break;
+            }
             // converged; or degenerate (rows whose slack and multiplier both vanish): complementarity 1e3 below
             // its tolerance while the dual residual stalls within 1e3 of its own, where the huge weights z/s
             // of those rows leave the Newton directions no more accurate than the iterate already is
@@ -1008,15 +1020,16 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         }
         p = nr;
         HSTAMP(7);
+        if (nonfin) break;
     }
     HSTAMP_FLUSH(b);
-    // non-finite result: zeros, LMPC_QP_NAN
+    // non-finite result or residuals: zeros, LMPC_QP_NAN
     bool bad = false;
     for (int l = 0; l < P.L; ++l)
         if (lane < P.n && !isfinite(xout[((int64_t)b * P.L + l) * P.n + lane])) bad = true;
     for (int r = lane; r < P.slack_len; r += 64)
         if (!isfinite(wout[(int64_t)b * P.slack_len + r])) bad = true;
-    if (__ballot(bad)) {
+    if (__ballot(bad) || nonfin) {
         for (int l = 0; l < P.L; ++l)
             if (lane < P.n) xout[((int64_t)b * P.L + l) * P.n + lane] = 0.0;
         for (int r = lane; r < P.slack_len; r += 64) wout[(int64_t)b * P.slack_len + r] = 0.0;

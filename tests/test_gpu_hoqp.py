@@ -227,3 +227,37 @@ def test_reference_ho_qp_test_program():
     exe = B.build_cpp_hoqp_test()
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and out.stdout.strip().endswith("ho_qp_test OK"), out.stdout + out.stderr
+
+
+def test_failure_statuses_stay_per_chain(hq):
+    """Failure detection per chain (include/lmpc/lmpc_hoqp.h, status): a record with a NaN gives LMPC_QP_NAN and
+    zeros without touching its neighbours (bitwise equal to a clean solve); an iteration cap gives LMPC_QP_MAX_ITER
+    with a finite iterate kept and the cap reported as the level's iteration count."""
+    g = load("wbc")
+    dims = dims_from(g["dims"])
+    rec = g["rec"].copy()
+    B = rec.shape[0]
+    solver = hq.HoqpBatch(dims, B)
+    x0, w0, st0, _ = solver.solve(rec)
+    assert np.all(st0 == 0)
+    bad = rec.copy()
+    # WBC record: level 0 a [0, 1260) b [1260, 1290) d [1290, 3138) f [3138, 3182); level 1 a, b from 3182;
+    # level 2 b [4460, 4472)
+    poisoned = {3: (100, np.nan), 5: (3150, np.nan), 7: (4465, np.nan), 9: (2000, np.inf), 11: (3190, -np.inf)}
+    for b, (i, v) in poisoned.items():
+        bad[b, i] = v
+    x, w, st, _ = solver.solve(bad)
+    for b in poisoned:
+        assert st[b] == 2 and np.all(x[b] == 0.0) and np.all(w[b] == 0.0), b
+    keep = np.array([b not in poisoned for b in range(B)])
+    assert np.all(st[keep] == 0)
+    assert np.array_equal(x[keep], x0[keep]) and np.array_equal(w[keep], w0[keep])
+    solver.set_options(max_iter=3)
+    try:
+        x, w, st, it = solver.solve(rec)
+        assert np.all(st == 1) and np.all(it <= 3) and np.any(it == 3)
+        assert np.all(np.isfinite(x)) and np.all(np.isfinite(w)) and np.all(w >= 0.0)
+    finally:
+        solver.set_options()
+    x, w, st, _ = solver.solve(rec)
+    assert np.all(st == 0) and np.array_equal(x, x0)
