@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
         DSTAMP(4);  // factorisation
         // ---- solve: U'y = r, U x = y (vectors replicated across the accumulator columns) ----
         {
-            d4 y[4], x[4];
+            d4 y[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
 #pragma unroll
@@ -316,12 +316,28 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             for (int b = 0; b < 4; ++b) {
                 if (b >= NT) continue;
                 d4 acc = y[b];
+                if (b > 0) {
+                    // t = sum_{a<b} U_ab' y_a on the VALU (a matrix-core product would use 1 of its 16 columns):
+                    // lane 16g + c sums U_ab[4i+g][c] y_a[4i+g] over its rows, then over the four row groups
+                    // -> t[c]; back to the replicated-across-columns layout through LDS
+                    double part = 0.0;
 #pragma unroll
-                for (int a = 0; a < b; ++a) acc = tprod_sub(Tl[tix(a, b)], y[a], acc);
+                    for (int a = 0; a < b; ++a) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) part = fma(Tl[tix(a, b)][i], y[a][i], part);
+                    }
+                    const double t = group_sum4(part);
+                    if (lr == 0) S.vec2[16 * b + lc] = t;
+                    LMPC_SYNC();
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i] -= S.vec2[16 * b + lr + 4 * i];
+                }
                 y[b] = tprod(Ui[b], acc, zero);
             }
             // backward: t = y_b - sum_c U_bc x_c on the VALU (x_c column-replicated: lane l holds
-            // x_c[l&15]; one DPP row sum per register), then x_b = U_bb^-1 t on the matrix cores
+            // x_c[l&15]; one DPP row sum per register), then x_b = U_bb^-1 t = UiT_b' t also on the VALU
+            // (lane 16g + c sums UiT_b[4i+g][c] t[4i+g], then over the row groups): x_b comes out
+            // column-replicated, which is the layout the tiles above read -- no LDS exchange
             double xcol[4];
 #pragma unroll
             for (int b = 3; b >= 0; --b) {
@@ -338,23 +354,16 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                     for (int i = 0; i < 4; ++i) acc[i] -= row_sum(part[i]);
                 }
-                x[b] = tprod(UiT[b], acc, zero);
-                if (b > 0) {  // column-replicated copy for the tiles above
-                    if (lc == 0) {
+                double p = 0.0;
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) S.vec2[16 * b + lr + 4 * i] = x[b][i];
-                    }
-                    LMPC_SYNC();
-                    xcol[b] = S.vec2[16 * b + lc];
-                }
+                for (int i = 0; i < 4; ++i) p = fma(UiT[b][i], acc[i], p);
+                xcol[b] = group_sum4(p);
             }
-            LMPC_SYNC();
-            if (lc == 0) {
+            if (lr == 0) {
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     if (b >= NT) continue;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) S.vec[16 * b + lr + 4 * i] = x[b][i];
+                    S.vec[16 * b + lc] = xcol[b];
                 }
             }
             LMPC_SYNC();

@@ -66,6 +66,35 @@ __device__ __forceinline__ double row_sum(double v) {
     return v;
 }
 
+// v + v(lane ^ W), W = 16 or 32: v_permlane{16,32}_swap of each dword with a copy of itself returns the lane's own
+// and its partner's value in its two outputs (which one is which depends on the half), so their sum needs no select.
+// The copy is opaque: with the same value in both operands hipcc (ROCm 7.2) merged the swaps of different
+// registers into one (tools/ubench/permlane_probe.hip).
+__device__ __forceinline__ unsigned opaque_u32(unsigned v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+template <int W>
+__device__ __forceinline__ double xor_pair_sum(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    unsigned l0, l1, h0, h1;
+    if constexpr (W == 32) {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, opaque_u32(lo), false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, opaque_u32(hi), false, false);
+        l0 = l[0]; l1 = l[1]; h0 = h[0]; h1 = h[1];
+    } else {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, opaque_u32(lo), false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, opaque_u32(hi), false, false);
+        l0 = l[0]; l1 = l[1]; h0 = h[0]; h1 = h[1];
+    }
+    const double d0 = __builtin_bit_cast(double, ((unsigned long long)h0 << 32) | l0);
+    const double d1 = __builtin_bit_cast(double, ((unsigned long long)h1 << 32) | l1);
+    return d0 + d1;
+}
+// sum over the four row groups (lanes c, 16+c, 32+c, 48+c); bitwise the same in all four (fp addition commutes)
+__device__ __forceinline__ double group_sum4(double v) { return xor_pair_sum<16>(xor_pair_sum<32>(v)); }
+
 struct DSmem {
     ldouble* hdr;   // 40: x0(12) R(9) feet(12)
     ldouble* G0;    // 72: B rows 6-11 (terrain: G0 blkdiag(R_j))

@@ -16,11 +16,19 @@ def pytest_configure(config):
 
 
 @pytest.fixture(scope="session", autouse=True)
-def _built():
-    """Build the HIP library and the oracle in-tree if they are missing (no-op when built)."""
+def _built(request):
+    """Build the HIP library and the oracle in-tree if they are missing (no-op when built).
+
+    When GPU tests are selected, torch's HIP runtime is brought up first: a selection whose first
+    GPU tests drive the C-ABI library alone (ctypes) initialised HIP before torch, and torch then
+    reported no device to the later tests that use it (seen with tests/test_gpu_parity.py run first)."""
     from legged_mpc_control_amd import build as B
     from oracle import oracle as O
 
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+
+        torch.cuda.is_available()
     B.build_native()
     O.build()
 
