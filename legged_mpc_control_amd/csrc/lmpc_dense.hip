@@ -305,34 +305,26 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
         DSTAMP(4);  // factorisation
         // ---- solve: U'y = r, U x = y (vectors replicated across the accumulator columns) ----
         {
+            // forward: y_b = U_bb^-T (r_b - sum_{a<b} U_ab' y_a), all on the VALU (a matrix-core product would use
+            // 1 of its 16 columns).  The bracket is column-indexed: lane 16g + c sums U_ab[4i+g][c] y_a[4i+g] over
+            // its rows, then over the four row groups -> t[c]; y_b = UiT_b (r_b - t) row by row (one DPP row sum
+            // per register) comes out replicated across the columns, the layout the next bracket reads.
             d4 y[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) y[b][i] = S.vec[16 * b + lr + 4 * i];
-            }
-            const d4 zero = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
                 if (b >= NT) continue;
-                d4 acc = y[b];
+                double acc = S.vec[16 * b + lc];
                 if (b > 0) {
-                    // t = sum_{a<b} U_ab' y_a on the VALU (a matrix-core product would use 1 of its 16 columns):
-                    // lane 16g + c sums U_ab[4i+g][c] y_a[4i+g] over its rows, then over the four row groups
-                    // -> t[c]; back to the replicated-across-columns layout through LDS
                     double part = 0.0;
 #pragma unroll
                     for (int a = 0; a < b; ++a) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) part = fma(Tl[tix(a, b)][i], y[a][i], part);
                     }
-                    const double t = group_sum4(part);
-                    if (lr == 0) S.vec2[16 * b + lc] = t;
-                    LMPC_SYNC();
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[i] -= S.vec2[16 * b + lr + 4 * i];
+                    acc -= group_sum4(part);
                 }
-                y[b] = tprod(Ui[b], acc, zero);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) y[b][i] = row_sum(UiT[b][i] * acc);
             }
             // backward: t = y_b - sum_c U_bc x_c on the VALU (x_c column-replicated: lane l holds
             // x_c[l&15]; one DPP row sum per register), then x_b = U_bb^-1 t = UiT_b' t also on the VALU
