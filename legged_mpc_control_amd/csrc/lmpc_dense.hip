@@ -40,11 +40,12 @@ namespace lmpc {
 
 // Diagnostic build only (-DLMPC_STAMPS): per-phase cycle counters of QP 0..4095 (tools/dense_check.py).
 #ifdef LMPC_STAMPS
-__device__ unsigned long long lmpc_dense_stamps[4096][8];
-#define DSTAMP_DECL unsigned long long _ds_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long _ds_t0 = __builtin_readcyclecounter();
+constexpr int DSTAMP_N = 12;
+__device__ unsigned long long lmpc_dense_stamps[4096][DSTAMP_N];
+#define DSTAMP_DECL unsigned long long _ds_acc[DSTAMP_N] = {}; unsigned long long _ds_t0 = __builtin_readcyclecounter();
 #define DSTAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _ds_acc[i] += _t - _ds_t0; _ds_t0 = _t; } while (0)
-#define DSTAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < 4096) for (int _i = 0; _i < 8; ++_i) lmpc_dense_stamps[qp][_i] = _ds_acc[_i]; } while (0)
-#define DS_PARAMS , unsigned long long (&_ds_acc)[8], unsigned long long& _ds_t0
+#define DSTAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < 4096) for (int _i = 0; _i < DSTAMP_N; ++_i) lmpc_dense_stamps[qp][_i] = _ds_acc[_i]; } while (0)
+#define DS_PARAMS , unsigned long long (&_ds_acc)[DSTAMP_N], unsigned long long& _ds_t0
 #define DS_ARGS , _ds_acc, _ds_t0
 #else
 #define DS_PARAMS
@@ -193,7 +194,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
         } else {
             LMPC_SYNC();
             // rhs = -T'(H up + g)
-            const double hv = h_matvec(S, S.vec2, NT, lane) + S.gv[lane];
+            const double hv = h_matvec(S, S.vec2, S.scr, lane) + S.gv[lane];
             LMPC_SYNC();
             S.vec2[lane] = hv;
             LMPC_SYNC();
@@ -208,7 +209,8 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             }
             LMPC_SYNC();
         }
-        DSTAMP(2);  // leg-step work + right-hand side (+ polish matvec)
+        if (mode == POLISH) DSTAMP(11);  // polish set-up + right-hand side (matvec)
+        else DSTAMP(2);                  // interior point: leg-step work + right-hand side
         if (mode != CORR) {
             // ---- M tiles ----
             if (mode == PRED) {
@@ -413,6 +415,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 cons_tw(wv, mu, rt);
             }
             mode = CORR;
+            DSTAMP(8);  // predictor step length + corrector terms
         } else if (mode == CORR) {
             double ds[5], dz[5];
             double amax = 1.0;
@@ -447,6 +450,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             }
             ++ipm_it;
             mode = PRED;
+            DSTAMP(9);  // corrector step + iterate update
         } else {
             // ---- polish verification: gradient H u + g, primal feasibility, multiplier signs ----
             S.vec2[lane] = 0.0;
@@ -456,7 +460,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 for (int p = 0; p < 3; ++p) S.vec2[vidx(lane, p)] = u[p];
             }
             LMPC_SYNC();
-            const double gl = h_matvec(S, S.vec2, NT, lane) + S.gv[lane];
+            const double gl = h_matvec(S, S.vec2, S.scr, lane) + S.gv[lane];
             LMPC_SYNC();
             S.vec2[lane] = gl;
             LMPC_SYNC();
@@ -498,6 +502,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                     }
                 }
             }
+            DSTAMP(10);  // polish verification
             if (!__any(changed)) {
                 done = true;
                 break;
@@ -561,7 +566,7 @@ template __global__ void lmpc_dense_kernel<true>(const DevParams, const double*,
 #ifdef LMPC_STAMPS
 extern "C" int lmpc_debug_dense_stamps(unsigned long long* out, int nqp) {
     if (nqp > 4096) nqp = 4096;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_dense_stamps), (size_t)nqp * 8 * sizeof(unsigned long long)) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_dense_stamps), (size_t)nqp * DSTAMP_N * sizeof(unsigned long long)) ==
                    hipSuccess ? nqp : -1;
 }
 #endif

@@ -425,22 +425,51 @@ __device__ __forceinline__ int tile_mask(const DSmem& S, int t, int nls, bool us
     return __builtin_amdgcn_readfirstlane(m);
 }
 
-// lane-wise y = H x for the variables (lane v = variable v), H from its upper tiles in LDS.
-// Lane v walks the columns starting at its own index, so a wave's reads spread over the banks.
-__device__ __forceinline__ double h_matvec(const DSmem& S, const ldouble* x, int NT, int lane) {
-    const int tv = lane >> 4, wv = lane & 15;
-    const int n = 16 * NT;
-    double acc = 0.0;
-    if (tv < NT) {
-        int w = lane;
-        for (int it = 0; it < n; ++it) {
-            w = (w + 1 == n) ? 0 : w + 1;
-            const int tw = w >> 4, ww = w & 15;
-            const int idx = (tv <= tw) ? tix(tv, tw) * DN_TILE + toff(wv, ww) : tix(tw, tv) * DN_TILE + toff(ww, wv);
-            acc = fma(S.Ht[idx], x[w], acc);
+// lane-wise y = H x for the variables (lane v = variable v; x in LDS by variable), H from its upper tiles in LDS,
+// as VALU tile products in the accumulator layout (lane 16g + c, register i <-> tile element (4i + g, c)):
+//   y_t gets T_rt' x_r for r <= t (the stored tile and the diagonal one): lane 16g + c sums T_rt[4i+g][c] x_r[4i+g]
+//       over its rows, then over the four row groups -> column-indexed (group_sum4);
+//   y_t gets T_tc x_c for c > t: lane 16g + c sums T_tc[4i+g][c] x_c[c] per register, then over its 16-lane row
+//       (row_sum) -> row-indexed, handed to lane order through tmp (64 doubles of LDS).
+// All loads are independent (one batch); until round 2 every lane walked its row of H with 64 dependent steps.
+__device__ __forceinline__ double h_matvec(const DSmem& S, const ldouble* x, ldouble* tmp, int lane) {
+    const int lc = lane & 15, lr = lane >> 4;
+    double xr[4][4], xc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[b][i] = x[16 * b + 4 * i + lr];
+        xc[b] = x[16 * b + lc];
+    }
+    double pc[4] = {0.0, 0.0, 0.0, 0.0};
+    double pr[3][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int c = r; c < 4; ++c) {
+            const int k = tix(r, c);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double h = S.Ht[k * DN_TILE + i * 64 + lane];
+                pc[c] = fma(h, xr[r][i], pc[c]);
+                if (c > r) pr[r][i] = fma(h, xc[c], pr[r][i]);
+            }
         }
     }
-    return acc;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const double v = row_sum(pr[r][i]);
+            if (lc == 0) tmp[16 * r + 4 * i + lr] = v;
+        }
+    }
+    double yc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) yc[c] = group_sum4(pc[c]);
+    LMPC_SYNC();
+    const double ys = lr == 0 ? yc[0] : lr == 1 ? yc[1] : lr == 2 ? yc[2] : yc[3];
+    return ys + (lr < 3 ? tmp[lane < 48 ? lane : 0] : 0.0);
 }
 
 // ---------------------------------------------------------------------------
