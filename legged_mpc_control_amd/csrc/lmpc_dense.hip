@@ -309,8 +309,9 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
         {
             // forward: y_b = U_bb^-T (r_b - sum_{a<b} U_ab' y_a), all on the VALU (a matrix-core product would use
             // 1 of its 16 columns).  The bracket is column-indexed: lane 16g + c sums U_ab[4i+g][c] y_a[4i+g] over
-            // its rows, then over the four row groups -> t[c]; y_b = UiT_b (r_b - t) row by row (one DPP row sum
-            // per register) comes out replicated across the columns, the layout the next bracket reads.
+            // its rows, then over the four row groups -> t[c]; y_b = UiT_b (r_b - t) row by row (the four
+            // registers' row sums at once, row_sum4) comes out replicated across the columns, the layout the
+            // next bracket reads.
             d4 y[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -325,11 +326,15 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                     }
                     acc -= group_sum4(part);
                 }
+                double pp[4], rs[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) y[b][i] = row_sum(UiT[b][i] * acc);
+                for (int i = 0; i < 4; ++i) pp[i] = UiT[b][i] * acc;
+                row_sum4(pp, rs);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) y[b][i] = rs[i];
             }
             // backward: t = y_b - sum_c U_bc x_c on the VALU (x_c column-replicated: lane l holds
-            // x_c[l&15]; one DPP row sum per register), then x_b = U_bb^-1 t = UiT_b' t also on the VALU
+            // x_c[l&15]; the four registers' row sums at once), then x_b = U_bb^-1 t = UiT_b' t also on the VALU
             // (lane 16g + c sums UiT_b[4i+g][c] t[4i+g], then over the row groups): x_b comes out
             // column-replicated, which is the layout the tiles above read -- no LDS exchange
             double xcol[4];
@@ -345,8 +350,10 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                         for (int i = 0; i < 4; ++i) part[i] = fma(Tl[tix(b, c)][i], xcol[c], part[i]);
                     }
+                    double rs[4];
+                    row_sum4(part, rs);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[i] -= row_sum(part[i]);
+                    for (int i = 0; i < 4; ++i) acc[i] -= rs[i];
                 }
                 double p = 0.0;
 #pragma unroll

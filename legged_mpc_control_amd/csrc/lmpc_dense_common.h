@@ -66,6 +66,27 @@ __device__ __forceinline__ double row_sum(double v) {
     return v;
 }
 
+// row_sum of four registers at once (each lane gets all four row totals): a transposing butterfly -- after the
+// xor-1 and xor-2 exchanges lane 4q + k holds the quad sum of p[k] only, two rotations finish the row, and a
+// quad broadcast per register hands every total back -- 35 instructions instead of four row_sums' 48.
+constexpr int DPP_QP_BC0 = 0x00, DPP_QP_BC1 = 0x55, DPP_QP_BC2 = 0xAA, DPP_QP_BC3 = 0xFF;  // quad_perm [k,k,k,k]
+__device__ __forceinline__ void row_sum4(const double p[4], double out[4]) {
+    const int lane = __lane_id();
+    const bool odd = lane & 1, hi2 = lane & 2;
+    const double sa = odd ? p[0] : p[1], sb = odd ? p[2] : p[3];
+    const double ka = odd ? p[1] : p[0], kb = odd ? p[3] : p[2];
+    const double s0 = ka + dpp_f64<DPP_QP_1032>(sa);  // p[lane & 1] over the pair
+    const double s1 = kb + dpp_f64<DPP_QP_1032>(sb);  // p[2 + (lane & 1)] over the pair
+    const double sc = hi2 ? s0 : s1, kc = hi2 ? s1 : s0;
+    double t = kc + dpp_f64<DPP_QP_2301>(sc);          // p[lane & 3] over the quad
+    t += dpp_f64<DPP_ROR4>(t);
+    t += dpp_f64<DPP_ROR8>(t);                          // ... over the row
+    out[0] = dpp_f64<DPP_QP_BC0>(t);
+    out[1] = dpp_f64<DPP_QP_BC1>(t);
+    out[2] = dpp_f64<DPP_QP_BC2>(t);
+    out[3] = dpp_f64<DPP_QP_BC3>(t);
+}
+
 // v + v(lane ^ W), W = 16 or 32: v_permlane{16,32}_swap of each dword with a copy of itself returns the lane's own
 // and its partner's value in its two outputs (which one is which depends on the half), so their sum needs no select.
 // The copy is opaque: with the same value in both operands hipcc (ROCm 7.2) merged the swaps of different
@@ -458,10 +479,11 @@ __device__ __forceinline__ double h_matvec(const DSmem& S, const ldouble* x, ldo
     }
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
+        double rs[4];
+        row_sum4(pr[r], rs);
+        if (lc == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const double v = row_sum(pr[r][i]);
-            if (lc == 0) tmp[16 * r + 4 * i + lr] = v;
+            for (int i = 0; i < 4; ++i) tmp[16 * r + 4 * i + lr] = rs[i];
         }
     }
     double yc[4];
