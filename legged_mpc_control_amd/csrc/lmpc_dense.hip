@@ -571,6 +571,11 @@ template __global__ void lmpc_dense_kernel<true>(const DevParams, const double*,
                                                  double*, int32_t*, int32_t*, uint8_t*);
 
 #ifdef LMPC_STAMPS
+extern "C" int lmpc_debug_condense_stamps(unsigned long long* out, int nqp) {
+    if (nqp > 4096) nqp = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_condense_stamps), (size_t)nqp * 5 * sizeof(unsigned long long)) ==
+                   hipSuccess ? nqp : -1;
+}
 extern "C" int lmpc_debug_dense_stamps(unsigned long long* out, int nqp) {
     if (nqp > 4096) nqp = 4096;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_dense_stamps), (size_t)nqp * DSTAMP_N * sizeof(unsigned long long)) ==

@@ -167,8 +167,19 @@ __device__ __forceinline__ DSmem dcarve(double* sm, int H) {
 // ---------------------------------------------------------------------------
 // Condensation: em, g, P~, H (see the header comment).  All lanes; lane v = variable v.
 // ---------------------------------------------------------------------------
+#ifdef LMPC_STAMPS
+// Diagnostic build only: cycles of the condensation's sub-phases per QP (tools/dense_check.py stamps).
+__device__ unsigned long long lmpc_condense_stamps[4096][5];
+#define CSTAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); \
+    if (lane == 0 && blockIdx.x < 4096) lmpc_condense_stamps[blockIdx.x][i] = _t - _cs_t0; _cs_t0 = _t; } while (0)
+#define CSTAMP_DECL unsigned long long _cs_t0 = __builtin_readcyclecounter();
+#else
+#define CSTAMP(i) do {} while (0)
+#define CSTAMP_DECL
+#endif
 __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem& S, int H, int nls, int lane) {
     const double dt = prm.dt;
+    CSTAMP_DECL
     // ---- free response and adjoint (every lane redundantly: no exchange needed) ----
     {
         double x[12];
@@ -192,6 +203,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
             }
         }
     }
+    CSTAMP(0);  // free response
     // variable of this lane
     const int vt = lane >> 4, vw = lane & 15;
     const int vb = 5 * vt + vw / 3, va = vw % 3;
@@ -231,6 +243,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
         }
         S.gv[lane] = gval;
     }
+    CSTAMP(1);  // adjoint + gradient
     // ---- P~ recursion on the matrix cores; store P~_m[:, 6:12] for m = 1..H ----
     {
         const int lc = lane & 15, lr = lane >> 4;
@@ -277,6 +290,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
             }
         }
     }
+    CSTAMP(2);  // P~ recursion
     // ---- H: zero tiles, identity on padding / unused slots, then one column per lane ----
 #pragma unroll 4
     for (int e = lane; e < 10 * DN_TILE; e += 64) S.Ht[e] = 0.0;
@@ -285,6 +299,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
         // identity on the diagonal of padding and unused variables (lane v = variable v)
         if (!vvalid) S.Ht[tix(vt, vt) * DN_TILE + toff(vw, vw)] = 1.0;
     }
+    CSTAMP(3);  // H zero + identity
     if (vvalid) {
         double L[12];
         const ldouble* Pt = S.scr + 72 * vk;  // P~_{k+1}
@@ -329,6 +344,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
         }
     }
     LMPC_SYNC();
+    CSTAMP(4);  // H columns
 }
 
 // ---------------------------------------------------------------------------

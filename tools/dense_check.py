@@ -82,6 +82,11 @@ def stamps():
         v = buf[:n, i].astype(float).mean()
         print(f"  {nm:20s} {v:10.0f} ({100 * v / tot.mean():5.1f}%)")
     print(f"  max cycles/QP {tot.max():.0f}, p99 {np.percentile(tot, 99):.0f}")
+    L.lmpc_debug_condense_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    cb = np.zeros((1024, 5), dtype=np.uint64)
+    n = L.lmpc_debug_condense_stamps(cb.ctypes.data, 1024)
+    for i, nm in enumerate(["free response", "adjoint + gradient", "P~ recursion", "H zero + identity", "H columns"]):
+        print(f"    condense: {nm:20s} {cb[:n, i].astype(float).mean():10.0f}")
     return tot
 
 
