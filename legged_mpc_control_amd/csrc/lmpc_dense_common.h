@@ -132,12 +132,12 @@ struct DSmem {
     ldouble* act;   // 20: 1 = leg-step coupled (T != 0)
     ldouble* lup;   // 60: polish particular solution up per leg-step (kept out of registers)
     ldouble* lua;   // 60: predictor step u_aff per leg-step
-    ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | diag_inverse: pivot rows (96) W' (272) sink (112)
+    ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | diag_inverse: T, W staging (256) W' (272) | h_matvec (48)
     lint* lsm;      // 20: stance leg-step b -> 4k + j
     lint* fb;       // H+1: first stance leg-step of step k
 };
 constexpr int DN_EL = 16 * 17;               // staging of one 16x16 tile, column stride 17
-constexpr int DN_SCR_MIN = 96 + DN_EL + 112;  // diag_inverse: pivot rows | W' | store sink
+constexpr int DN_SCR_MIN = 256 + DN_EL;  // diag_inverse: staging of T and W (128 each) | W'
 
 __device__ __forceinline__ DSmem dcarve(double* sm, int H) {
     DSmem s;
@@ -354,7 +354,8 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
 //
 // The tile T and W = L^-1 (from I) stay in the MFMA accumulator layout (lane 16g + c, register i <->
 // element (4i + g, c)).  Per pivot block P = T[o..o+2][o..o+2] (o = 3 blk):
-//   the three pivot rows of T and W go through LDS once (one write -> read round trip);
+//   the registers holding the three pivot rows of T and W go through LDS once (one write -> read round trip;
+//   every lane stores, so the reads have static offsets);
 //   every lane factors P = L_p L_p' itself (3 rsq + Newton);
 //   lane 16k + m forms L_C[m][k] = (L_p^-1 T[o..o+2][m])_k for the rows m below the pivot (T symmetric)
 //   and (L_p^-1 W[o..o+2][c])_k -- the MFMA A and B operands;
@@ -370,9 +371,11 @@ struct DiagInv {
 // competing with the factor tiles and the leg state that are live around it.
 static __device__ __attribute__((noinline)) DiagInv diag_inverse(ldouble* scr, d4 M, int amask, int lane) {
     amask = __builtin_amdgcn_readfirstlane(amask);  // uniform (tile_mask), but arguments arrive in VGPRs
-    ldouble* pv = scr;              // 96: pivot rows o..o+2 of T (48) then of W (48), 16 columns each
-    ldouble* tr = scr + 96;         // 16 x 17: transpose staging of W
-    ldouble* dummy = scr + 96 + 272;  // 112: sink of the stores of lanes that hold no pivot row
+    // staging of the registers that hold the pivot rows (i0, i1): every lane stores its value unconditionally, so
+    // row r of register i sits at 16 (r & 3) + c (+64 for i1) -- static read offsets, no per-lane address select
+    ldouble* sT = scr;        // 128: T
+    ldouble* sW = scr + 128;  // 128: W
+    ldouble* tr = scr + 256;  // 16 x 17: transpose staging of W
     const int c = lane & 15, g = lane >> 4;
     d4 T = M, W;
 #pragma unroll
@@ -385,40 +388,35 @@ static __device__ __attribute__((noinline)) DiagInv diag_inverse(ldouble* scr, d
         const int i0 = o >> 2, i1 = (o + 2) >> 2;
         const int ra = 4 * i0 + g - o, rb = 4 * i1 + g - o;
         const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
+        // staging offset of pivot row o+a (static)
+        auto so = [&](int a) { return ((o + a) >> 2 == i0 ? 0 : 64) + 16 * ((o + a) & 3); };
         LMPC_SYNC();
-        // publish the pivot rows of T first (unconditional stores; lanes without a pivot row store to the sink):
-        // the T chain of this pivot waits only for the previous T update, not for the W update issued after it
-        {
-            ldouble* da = ina ? pv + 16 * ra + c : dummy + lane;
-            da[0] = T[i0];
-            if (i1 != i0) {
-                ldouble* db = inb ? pv + 16 * rb + c : dummy + lane;
-                db[0] = T[i1];
-            }
-        }
+        // publish the registers of T first: the T chain of this pivot waits only for the previous T update
+        sT[lane] = T[i0];
+        if (i1 != i0) sT[64 + lane] = T[i1];
         LMPC_SYNC();
-        const double p00 = pv[o], p10 = pv[16 + o], p11 = pv[16 + o + 1];
-        const double p20 = pv[32 + o], p21 = pv[32 + o + 1], p22 = pv[32 + o + 2];
-        const double t0 = pv[c], t1 = pv[16 + c], t2 = pv[32 + c];               // T[o+a][c] = T[c][o+a]
-        // then the pivot rows of W (+48), read while the pivot is factored; W's pivot rows are cleared so the
-        // MFMA below writes L_p^-1 W_p into them
-        {
-            ldouble* da = ina ? pv + 48 + 16 * ra + c : dummy + 48 + lane;
-            da[0] = W[i0];
-            W[i0] = ina ? 0.0 : W[i0];
-            if (i1 != i0) {
-                ldouble* db = inb ? pv + 48 + 16 * rb + c : dummy + 48 + lane;
-                db[0] = W[i1];
-                W[i1] = inb ? 0.0 : W[i1];
-            }
-        }
+        const double p00 = sT[so(0) + o], p10 = sT[so(1) + o], p11 = sT[so(1) + o + 1];
+        const double p20 = sT[so(2) + o], p21 = sT[so(2) + o + 1], p22 = sT[so(2) + o + 2];
+        const double t0 = sT[so(0) + c], t1 = sT[so(1) + c], t2 = sT[so(2) + c];  // T[o+a][c] = T[c][o+a]
+        // then those of W, read while the pivot is factored; W's pivot rows are cleared so the MFMA below writes
+        // L_p^-1 W_p into them
+        sW[lane] = W[i0];
+        if (i1 != i0) sW[64 + lane] = W[i1];
+        W[i0] = ina ? 0.0 : W[i0];
+        if (i1 != i0) W[i1] = inb ? 0.0 : W[i1];
         LMPC_SYNC();
-        const double w0 = pv[48 + c], w1 = pv[64 + c], w2 = pv[80 + c];          // W[o+a][c]
-        const double i00 = rsq_nr(p00);
+        const double w0 = sW[so(0) + c], w1 = sW[so(1) + c], w2 = sW[so(2) + c];  // W[o+a][c]
+        // P = L_p L_p' with the three pivot reciprocals from the leading minors, so their rsq chains run side by
+        // side instead of one after the other: d1 = m11 / p00, d2 = det / m11 (m11 = p00 p11 - p10^2), hence
+        // 1/sqrt(d1) = sqrt(p00) rsq(m11) and 1/sqrt(d2) = sqrt(m11) rsq(det)
+        const double m11 = fma(p00, p11, -p10 * p10);
+        const double c00 = fma(p11, p22, -p21 * p21), c01 = fma(p10, p22, -p21 * p20), c02 = fma(p10, p21, -p11 * p20);
+        const double det = fma(p00, c00, fma(-p10, c01, p20 * c02));
+        const double i00 = rsq_nr(p00), r1 = rsq_nr(m11), r2 = rsq_nr(det);
         const double l10 = p10 * i00, l20 = p20 * i00;
-        const double i11 = rsq_nr(fma(-l10, l10, p11));
+        const double i11 = (p00 * i00) * r1;
         const double l21 = fma(-l20, l10, p21) * i11;
-        const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
+        const double i22 = (m11 * r1) * r2;
         // row c of L_C (zero in and above the pivot rows)
         const double x0 = t0 * i00;
         const double x1 = fma(-l10, x0, t1) * i11;

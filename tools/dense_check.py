@@ -82,6 +82,9 @@ def stamps():
         v = buf[:n, i].astype(float).mean()
         print(f"  {nm:20s} {v:10.0f} ({100 * v / tot.mean():5.1f}%)")
     print(f"  max cycles/QP {tot.max():.0f}, p99 {np.percentile(tot, 99):.0f}")
+    for q in np.argsort(-tot)[:6]:
+        print(f"    slow QP {q}: {tot[q]:.0f} cycles, ipm {it[q] & 0xffff} rounds {it[q] >> 16}, "
+              f"diag {buf[q, 6]:.0f} solve {buf[q, 5]:.0f}")
     L.lmpc_debug_condense_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     cb = np.zeros((1024, 5), dtype=np.uint64)
     n = L.lmpc_debug_condense_stamps(cb.ctypes.data, 1024)

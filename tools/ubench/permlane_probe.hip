@@ -1,6 +1,6 @@
-// Probe of the gfx950 cross-row swaps used by diag_inverse's tile_row (lmpc_dense_common.h):
+// Probe of the gfx950 cross-row swaps used by the dense path's group_sum4 (lmpc_dense_common.h):
 //  (1) which source row each output of v_permlane16_swap / v_permlane32_swap holds;
-//  (2) tile_row / tile_at on a tile produced by an MFMA and consumed at once (hazards), checked per lane;
+//  (2) group_sum4 / row_sum4 (the solves' cross-lane sums), checked per lane against the host;
 //  (3) diag_inverse on an SPD tile: max |L^-1 M L^-T - I| (host check).
 #include "../../legged_mpc_control_amd/csrc/lmpc_dense.hip"
 
@@ -17,23 +17,15 @@ __global__ void probe(unsigned* out) {
     out[3 * 64 + x] = s32[1];
 }
 
-// tile X = A'B through one MFMA (A = lane-valued, B = identity-ish), then every row broadcast / element read at once
-__global__ void rows_probe(double* out, double* el) {
-    const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
-    lmpc::d4 X = {0.0, 0.0, 0.0, 0.0};
-    // A[m][k] (lane: m = lane&15, k = lane>>4) = 1 + m + 100k; B[k][n] = (k == 0 && n == ...) -> X[m][n] = sum_k A[k][m] B[k][n]
-    const double a = 1.0 + c + 100.0 * g, b = 1.0 + 0.5 * c + 7.0 * g;
-    X = MFMA64(a, b, X);
-    double r[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) r[q] = lmpc::tile_row(X, q);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) out[q * 64 + lane] = r[q];
-    double e[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) e[q] = lmpc::tile_at(X, q, (q * 5) & 15);
-    if (lane == 0)
-        for (int q = 0; q < 16; ++q) el[q] = e[q];
+// group_sum4 and row_sum4 (lmpc_dense_common.h) on lane-valued data, every lane checked on the host
+__global__ void sums_probe(double* out) {
+    const int lane = threadIdx.x;
+    const double v = 1.0 + lane + 0.001 * lane * lane;
+    out[lane] = lmpc::group_sum4(v);
+    double p[4], r[4];
+    for (int k = 0; k < 4; ++k) p[k] = v * (k + 1) + k;
+    lmpc::row_sum4(p, r);
+    for (int k = 0; k < 4; ++k) out[64 * (k + 1) + lane] = r[k];
 }
 
 __global__ void __launch_bounds__(64) diag_check(const double* Min, double* Wout) {
@@ -59,32 +51,28 @@ int main() {
         printf("\n");
     }
     // (2)
-    double *dr, *de, hr[16 * 64], he[16];
-    (void)hipMalloc(&dr, sizeof(hr));
-    (void)hipMalloc(&de, sizeof(he));
-    hipLaunchKernelGGL(rows_probe, dim3(1), dim3(64), 0, 0, dr, de);
-    (void)hipMemcpy(hr, dr, sizeof(hr), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(he, de, sizeof(he), hipMemcpyDeviceToHost);
-    double X[16][16];
-    for (int m = 0; m < 16; ++m)
-        for (int n = 0; n < 16; ++n) {
-            double s = 0.0;
-            for (int k = 0; k < 4; ++k) s += (1.0 + m + 100.0 * k) * (1.0 + 0.5 * n + 7.0 * k);
-            X[m][n] = s;
+    double *ds, hs[5 * 64];
+    (void)hipMalloc(&ds, sizeof(hs));
+    hipLaunchKernelGGL(sums_probe, dim3(1), dim3(64), 0, 0, ds);
+    (void)hipMemcpy(hs, ds, sizeof(hs), hipMemcpyDeviceToHost);
+    double worst = 0.0;
+    for (int l = 0; l < 64; ++l) {
+        double gs = 0.0;
+        for (int g = 0; g < 4; ++g) {
+            const int m = 16 * g + (l & 15);
+            gs += 1.0 + m + 0.001 * m * m;
         }
-    int bad = 0;
-    for (int q = 0; q < 16; ++q)
-        for (int l = 0; l < 64; ++l)
-            if (hr[q * 64 + l] != X[q][l & 15]) {
-                if (bad < 8) printf("tile_row(%d) lane %d: %g expected %g\n", q, l, hr[q * 64 + l], X[q][l & 15]);
-                ++bad;
+        worst = fmax(worst, fabs(hs[l] - gs) / gs);
+        for (int k = 0; k < 4; ++k) {
+            double rs = 0.0;
+            for (int c = 0; c < 16; ++c) {
+                const int m = 16 * (l >> 4) + c;
+                rs += (1.0 + m + 0.001 * m * m) * (k + 1) + k;
             }
-    for (int q = 0; q < 16; ++q)
-        if (he[q] != X[q][(q * 5) & 15]) {
-            if (bad < 16) printf("tile_at(%d,%d): %g expected %g\n", q, (q * 5) & 15, he[q], X[q][(q * 5) & 15]);
-            ++bad;
+            worst = fmax(worst, fabs(hs[64 * (k + 1) + l] - rs) / rs);
         }
-    printf("tile_row/tile_at after an MFMA: %d mismatches\n", bad);
+    }
+    printf("group_sum4 / row_sum4: max relative error %.3e over all lanes\n", worst);
     // (3)
     double Mh[256], Wh[256];
     for (int r = 0; r < 16; ++r)
@@ -98,7 +86,7 @@ int main() {
     (void)hipFuncSetAttribute((const void*)diag_check, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(diag_check, dim3(1), dim3(64), lds, 0, dM, dW);
     (void)hipMemcpy(Wh, dW, sizeof(Wh), hipMemcpyDeviceToHost);
-    double worst = 0.0;
+    worst = 0.0;
     for (int i = 0; i < 16; ++i)
         for (int j = 0; j < 16; ++j) {
             double s = 0.0;  // (W M W')_ij
