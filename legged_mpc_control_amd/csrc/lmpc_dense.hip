@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 
     const int rank = dense_prologue<TERRAIN>(prm, S, rec, normals, qp, H, smask, stl, lane);
     DSTAMP(0);  // prologue
-    dense_condense(prm, S, H, nls, lane);
+    dense_condense<TERRAIN>(prm, S, H, nls, lane);
     // Always four tiles: leg-steps beyond nls are identity padding (exact, and it keeps every tile
     // index static, so register liveness is exact across the predictor / corrector solves).
     constexpr int NT = 4;
@@ -118,6 +118,9 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
     // first attempt: at most dense_polish_iter interior-point iterations before the polish (the polish verifies
     // the optimum exactly; a failed polish resumes the interior point with a tighter tolerance below)
     int att = 0, rd = 0, it_end = min(prm.max_iter, prm.dense_polish_iter), mode = PRED, act = 0;
+    // polish rounds after a polish round: diagonal tiles before the first leg-step whose active set changed keep their
+    // factors (their M tiles, and every panel and update feeding them, are bitwise those of the previous round)
+    int keep_tiles = 0;
     bool apex = false;
     double mu_c = 0.0, smu = 0.0;
     // factor tiles (register resident through the corrector): U's off-diagonal tiles in Tl, U_bb^-1, U_bb^-T
@@ -143,6 +146,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 }
                 mode = POLISH;
                 rd = 0;
+                keep_tiles = 0;
             } else {
                 double W[5] = {0, 0, 0, 0, 0}, wv[5] = {0, 0, 0, 0, 0};
                 if (st) {
@@ -281,7 +285,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             for (int b = 0; b < 4; ++b) {
                 if (b >= NT) continue;
                 DSTAMP(4);
-                {
+                if (b >= keep_tiles) {
                     const DiagInv di = diag_inverse(S.scr, Tl[tix(b, b)], tile_mask(S, b, nls, mode == POLISH), lane);
                     Ui[b] = di.ui;
                     UiT[b] = di.uit;
@@ -510,11 +514,14 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 }
             }
             DSTAMP(10);  // polish verification
-            if (!__any(changed)) {
+            const unsigned long long chg = __ballot(changed);
+            if (!chg) {
                 done = true;
                 break;
             }
+            keep_tiles = (__ffsll((long long)chg) - 1) / 5;  // tile of the first changed leg-step
             if (++rd >= prm.max_rounds) {
+                keep_tiles = 0;
                 if (++att >= prm.max_attempts) break;
                 tol *= 1e-3;
                 it_end += prm.max_iter;

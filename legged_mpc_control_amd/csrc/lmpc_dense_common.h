@@ -177,6 +177,7 @@ __device__ unsigned long long lmpc_condense_stamps[4096][5];
 #define CSTAMP(i) do {} while (0)
 #define CSTAMP_DECL
 #endif
+template <bool TERRAIN>
 __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem& S, int H, int nls, int lane) {
     const double dt = prm.dt;
     CSTAMP_DECL
@@ -301,6 +302,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
     }
     CSTAMP(3);  // H zero + identity
     if (vvalid) {
+        const double dtm = dt / prm.mass;
         double L[12];
         const ldouble* Pt = S.scr + 72 * vk;  // P~_{k+1}
         double gc[6];
@@ -332,8 +334,14 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
                 for (int ap = 0; ap < 3; ++ap) {
                     const int cp = 3 * jp + ap;
                     double val = 0.0;
+                    if constexpr (TERRAIN) {
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+                        for (int q = 0; q < 6; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+                    } else {  // flat ground: rows 3-5 of G0 are dt/m I (dense_prologue) -- the same sum, bit for bit
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+                        val = fma(dtm, L[9 + ap], val);
+                    }
                     if (bp == vb) val += S.rb[6 * vj + sym3(ap, va)];
                     const int vp = vidx(bp, ap);
                     const int tp = vp >> 4;
