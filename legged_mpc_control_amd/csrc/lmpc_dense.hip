@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
     int qstatus = LMPC_QP_CONVERGED, ipm_it = 0, prounds = 0;
     bool done = false;
     enum { PRED = 0, CORR = 1, POLISH = 2 };
-    const double mc = 5.0 * nls;
+    const double mc = 5.0 * nls, imc = 1.0 / mc;  // complementarity pairs
     double tol = prm.tol_mu;
     // first attempt: at most dense_polish_iter interior-point iterations before the polish (the polish verifies
     // the optimum exactly; a failed polish resumes the interior point with a tighter tolerance below)
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
     // factors (their M tiles, and every panel and update feeding them, are bitwise those of the previous round)
     int keep_tiles = 0;
     bool apex = false;
-    double mu_c = 0.0, smu = 0.0;
+    double mu_c = 0.0, smu = 0.0, sz = 0.0;  // sz = sum of s'z at the iterate (mu_c = sz / mc)
     // factor tiles (register resident through the corrector): U's off-diagonal tiles in Tl, U_bb^-1, U_bb^-T
     d4 Tl[10], Ui[4], UiT[4];
     const int lc = lane & 15, lr = lane >> 4;
@@ -134,7 +134,8 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                 for (int i = 0; i < 5; ++i) loc += s[i] * z[i];
             }
-            mu_c = wave_sum(loc) / mc;
+            sz = wave_sum(loc);
+            mu_c = sz * imc;
             if (mu_c < tol || ipm_it >= it_end) {
                 act = 0;
                 if (st) {
@@ -416,7 +417,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                 for (int i = 0; i < 5; ++i) loc += (s[i] + aa * dsa[i]) * (z[i] + aa * dza[i]);
             }
-            const double ratio = (wave_sum(loc) / mc) / mu_c;
+            const double ratio = wave_sum(loc) / sz;  // = mu_aff / mu (the 1/mc factors cancel)
             smu = ratio * ratio * ratio * mu_c;
             if (st) {
                 double wv[5];
