@@ -274,7 +274,10 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                         const bool dg = r == lc && r < 15 && bb < nls;
                         const ldouble* bk = S.blk + 9 * (dg ? bb : 0);
                         const int a = r % 3;
-                        const bool fixed = bk[a] == 0.0 && bk[3 + a] == 0.0 && bk[6 + a] == 0.0;
+                        // all three loads, then bitwise ands: a short-circuit && compiled to three branches, each
+                        // waiting on its own LDS load, for every element of the diagonal tiles
+                        const double b0 = bk[a], b1 = bk[3 + a], b2 = bk[6 + a];
+                        const bool fixed = (b0 == 0.0) & (b1 == 0.0) & (b2 == 0.0);
                         Tl[tix(t, t)][i] += (dg && fixed) ? 1.0 : 0.0;
                     }
                 }

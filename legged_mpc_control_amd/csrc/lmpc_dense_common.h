@@ -463,7 +463,8 @@ __device__ __forceinline__ int tile_mask(const DSmem& S, int t, int nls, bool us
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
         const int b = 5 * t + s;
-        if (b < nls && (!use_act || S.act[b < 20 ? b : 0] != 0.0)) m |= 1 << s;
+        const double a = S.act[b < 20 ? b : 0];  // loaded unconditionally: no branch waits on it
+        m |= ((b < nls) & (!use_act | (a != 0.0))) << s;
     }
     return __builtin_amdgcn_readfirstlane(m);
 }
