@@ -40,7 +40,7 @@ namespace lmpc {
 
 // Diagnostic build only (-DLMPC_STAMPS): per-phase cycle counters of QP 0..4095 (tools/dense_check.py).
 #ifdef LMPC_STAMPS
-constexpr int DSTAMP_N = 12;
+constexpr int DSTAMP_N = 14;
 __device__ unsigned long long lmpc_dense_stamps[4096][DSTAMP_N];
 #define DSTAMP_DECL unsigned long long _ds_acc[DSTAMP_N] = {}; unsigned long long _ds_t0 = __builtin_readcyclecounter();
 #define DSTAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _ds_acc[i] += _t - _ds_t0; _ds_t0 = _t; } while (0)
@@ -134,8 +134,10 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                 for (int i = 0; i < 5; ++i) loc += s[i] * z[i];
             }
+            DSTAMP(2);
             sz = wave_sum(loc);
             mu_c = sz * imc;
+            DSTAMP(12);  // complementarity mean (wave reduction)
             if (mu_c < tol || ipm_it >= it_end) {
                 act = 0;
                 if (st) {
@@ -167,6 +169,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 }
                 cons_tw(wv, mu, rt);
             }
+            DSTAMP(13);  // Newton-matrix blocks D and weights
         }
         if (mode == POLISH) {
             ++prounds;

@@ -72,11 +72,12 @@ def stamps():
     g, st, it = s.solve(rec, con)
     L = N.lib()
     L.lmpc_debug_dense_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = np.zeros((1024, 12), dtype=np.uint64)
+    buf = np.zeros((1024, 14), dtype=np.uint64)
     n = L.lmpc_debug_dense_stamps(buf.ctypes.data, 1024)
     names = ["prologue", "condense", "ipm leg-step + rhs", "M tiles (ipm)", "factor (MFMA part)", "solve", "diag tiles",
-             "M tiles (polish)", "predictor step", "corrector step", "polish verify", "polish set-up + rhs"]
-    tot = buf[:n, :12].sum(1).astype(float)
+             "M tiles (polish)", "predictor step", "corrector step", "polish verify", "polish set-up + rhs",
+             "ipm: wave_sum of s'z", "ipm: D blocks + weights"]
+    tot = buf[:n, :14].sum(1).astype(float)
     print(f"dense config 2: mean cycles/QP {tot.mean():.0f} (ipm {np.mean(it & 0xffff):.2f} rounds {np.mean(it >> 16):.2f})")
     for i, nm in enumerate(names):
         v = buf[:n, i].astype(float).mean()
