@@ -126,6 +126,20 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
     // factor tiles (register resident through the corrector): U's off-diagonal tiles in Tl, U_bb^-1, U_bb^-T
     d4 Tl[10], Ui[4], UiT[4];
     const int lc = lane & 15, lr = lane >> 4;
+    // Diagonal-tile elements inside a 3x3 leg block: lane 16 lr + lc holds rows lr + 4i of column lc, and at most one
+    // of them (register lblk_reg, -1 if none) lies in lc's block (rows 3 lblk_q .. 3 lblk_q + 2); lblk_off is its
+    // offset in the leg-step's 9-entry block of S.blk
+    int lblk_reg = -1, lblk_q = 0, lblk_off = 0, ldg_reg = -1;  // ldg_reg: the register holding element (lc, lc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        if (r < 15 && lc < 15 && r / 3 == lc / 3) {
+            lblk_reg = i;
+            lblk_q = r / 3;
+            lblk_off = 3 * (r % 3) + lc % 3;
+            if (r == lc) ldg_reg = i;
+        }
+    }
     for (;;) {
         if (mode == PRED) {
             if (ipm_it >= prm.dense_iter_cap) break;  // test hook: hand the QP to the Riccati kernel
@@ -227,31 +241,26 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 #pragma unroll
                     for (int i = 0; i < 4; ++i) Tl[t][i] = S.Ht[t * DN_TILE + i * 64 + lane];
                 }
-                // + D on the diagonal leg blocks
+                // + D on the diagonal leg blocks: one load per tile (lblk_reg below)
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
+                    const int bb = 5 * t + lblk_q;
+                    const bool inb = lblk_reg >= 0 && bb < nls;
+                    const double d = S.blk[inb ? 9 * bb + lblk_off : 0];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = lr + 4 * i;
-                        const int bb = 5 * t + r / 3;
-                        const bool inb = r < 15 && lc < 15 && (r / 3) == (lc / 3) && bb < nls;
-                        const double d = S.blk[inb ? 9 * bb + 3 * (r % 3) + (lc % 3) : 0];
-                        Tl[tix(t, t)][i] += inb ? d : 0.0;
-                    }
+                    for (int i = 0; i < 4; ++i) Tl[tix(t, t)][i] += (inb && i == lblk_reg) ? d : 0.0;
                 }
             } else {
                 // polish: T^ tiles (block diagonal; identity on unused / padding slots)
                 d4 Th[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
+                    const int bb = 5 * t + lblk_q;
+                    const bool inb = lblk_reg >= 0 && bb < nls;
+                    const double tv = S.blk[inb ? 9 * bb + lblk_off : 0];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = lr + 4 * i;
-                        const int bb = 5 * t + r / 3;
-                        const bool inb = r < 15 && lc < 15 && (r / 3) == (lc / 3) && bb < nls;
-                        const double tv = S.blk[inb ? 9 * bb + 3 * (r % 3) + (lc % 3) : 0];
-                        Th[t][i] = inb ? tv : (r == lc ? 1.0 : 0.0);
-                    }
+                    for (int i = 0; i < 4; ++i)
+                        Th[t][i] = (inb && i == lblk_reg) ? tv : (lr + 4 * i == lc ? 1.0 : 0.0);
                 }
                 // Tl(tr, tc) = T^_tr' H_tr,tc T^_tc  (two X'Y products per tile)
 #pragma unroll
@@ -267,22 +276,19 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                         Tl[tix(tr, tc)] = tprod(Yt, Th[tc], zero);
                     }
                 }
-                // + identity on fixed components (zero T columns) of the diagonal leg blocks
+                // + identity on fixed components (zero T columns) of the diagonal leg blocks: the lane's own diagonal
+                // element (register ldg_reg, if it holds one) -- one test per tile
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
+                    const int bb = 5 * t + lblk_q;
+                    const bool dg = ldg_reg >= 0 && bb < nls;
+                    const ldouble* bk = S.blk + 9 * (dg ? bb : 0);
+                    const int a = lc % 3;
+                    // all three loads, then bitwise ands (a short-circuit && waited on each load in turn)
+                    const double b0 = bk[a], b1 = bk[3 + a], b2 = bk[6 + a];
+                    const bool fixed = dg & (b0 == 0.0) & (b1 == 0.0) & (b2 == 0.0);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = lr + 4 * i;
-                        const int bb = 5 * t + r / 3;
-                        const bool dg = r == lc && r < 15 && bb < nls;
-                        const ldouble* bk = S.blk + 9 * (dg ? bb : 0);
-                        const int a = r % 3;
-                        // all three loads, then bitwise ands: a short-circuit && compiled to three branches, each
-                        // waiting on its own LDS load, for every element of the diagonal tiles
-                        const double b0 = bk[a], b1 = bk[3 + a], b2 = bk[6 + a];
-                        const bool fixed = (b0 == 0.0) & (b1 == 0.0) & (b2 == 0.0);
-                        Tl[tix(t, t)][i] += (dg && fixed) ? 1.0 : 0.0;
-                    }
+                    for (int i = 0; i < 4; ++i) Tl[tix(t, t)][i] += (fixed && i == ldg_reg) ? 1.0 : 0.0;
                 }
             }
             if (mode == POLISH) DSTAMP(7);  // M tiles (polish)
