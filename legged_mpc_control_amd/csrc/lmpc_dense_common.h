@@ -217,6 +217,13 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
         vj = id & 3;
     }
     const int vc = 3 * vj + va;
+    // this variable's column of B (rows 6-11: G0) and its leg's input-Hessian row, loaded once up front (inside the
+    // step loops they were loads under divergent branches, each waiting for its own LDS round trip)
+    double gc[6], rbl[3];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) gc[q] = S.G0[q * 12 + vc];
+#pragma unroll
+    for (int ap = 0; ap < 3; ++ap) rbl[ap] = S.rb[6 * vj + sym3(ap, va)];
     {
         double mu[12];
 #pragma unroll
@@ -238,7 +245,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
             if (vvalid && vk + 1 == m) {
                 double gs = 0.0;
 #pragma unroll
-                for (int q = 0; q < 6; ++q) gs += S.G0[q * 12 + vc] * mu[6 + q];
+                for (int q = 0; q < 6; ++q) gs += gc[q] * mu[6 + q];
                 gval = gs;
             }
         }
@@ -305,9 +312,6 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
         const double dtm = dt / prm.mass;
         double L[12];
         const ldouble* Pt = S.scr + 72 * vk;  // P~_{k+1}
-        double gc[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) gc[q] = S.G0[q * 12 + vc];
 #pragma unroll
         for (int r = 0; r < 12; ++r) {
             double acc = 0.0;
@@ -342,7 +346,7 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
                         for (int q = 0; q < 3; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
                         val = fma(dtm, L[9 + ap], val);
                     }
-                    if (bp == vb) val += S.rb[6 * vj + sym3(ap, va)];
+                    if (bp == vb) val += rbl[ap];
                     const int vp = vidx(bp, ap);
                     const int tp = vp >> 4;
                     if (tp <= vt) S.Ht[tix(tp, vt) * DN_TILE + toff(vp & 15, vw)] = val;
