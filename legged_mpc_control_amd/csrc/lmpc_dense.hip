@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
 
     const int rank = dense_prologue<TERRAIN>(prm, S, rec, normals, qp, H, smask, stl, lane);
     DSTAMP(0);  // prologue
-    dense_condense<TERRAIN>(prm, S, H, nls, lane);
+    dense_condense<TERRAIN>(prm, S, H, nls, smask, lane);
     // Always four tiles: leg-steps beyond nls are identity padding (exact, and it keeps every tile
     // index static, so register liveness is exact across the predictor / corrector solves).
     constexpr int NT = 4;

@@ -178,7 +178,8 @@ __device__ unsigned long long lmpc_condense_stamps[4096][5];
 #define CSTAMP_DECL
 #endif
 template <bool TERRAIN>
-__device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem& S, int H, int nls, int lane) {
+__device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem& S, int H, int nls,
+                                               unsigned long long smask, int lane) {
     const double dt = prm.dt;
     CSTAMP_DECL
     // ---- free response and adjoint (every lane redundantly: no exchange needed) ----
@@ -308,20 +309,27 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
         if (!vvalid) S.Ht[tix(vt, vt) * DN_TILE + toff(vw, vw)] = 1.0;
     }
     CSTAMP(3);  // H zero + identity
-    if (vvalid) {
+    {
+        // Column v of H (this lane's variable: leg-step vb at step vk, leg vj, component va):
+        //   L_i = (A_vk ... A_{i+1})' P~_{vk+1} B e_v for i = vk..0, and H[v'][v] = G0_j'^T L_i[6:12] for the stance
+        //   variables v' of step i (+ R on the own 3x3 block).  The step loop is uniform (lanes with vk < i idle):
+        //   the stance legs of step i come from the ballot (smask: bit 4k+j) in scalar registers, so no LDS load
+        //   (first leg-step of the step, leg of the leg-step) sits ahead of the G0 loads.
         const double dtm = dt / prm.mass;
         double L[12];
-        const ldouble* Pt = S.scr + 72 * vk;  // P~_{k+1}
+        {
+            const ldouble* Pt = S.scr + 72 * vk;  // P~_{k+1}
 #pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            double acc = 0.0;
+            for (int r = 0; r < 12; ++r) {
+                double acc = 0.0;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) acc = fma(Pt[6 * r + q], gc[q], acc);
-            L[r] = acc;
+                for (int q = 0; q < 6; ++q) acc = fma(Pt[6 * r + q], gc[q], acc);
+                L[r] = acc;
+            }
         }
-        const int v = lane;
-        for (int i = vk; i >= 0; --i) {
-            if (i < vk) {  // L <- A_{i+1}' L
+        const int vkk = vvalid ? vk : -1;  // padding / unused lanes take part in no step
+        for (int i = H - 1; i >= 0; --i) {
+            if (i < vkk) {  // L <- A_{i+1}' L
                 const double ck = S.cs[2 * (i + 1)], sk = S.cs[2 * (i + 1) + 1];
                 const double l0 = L[0], l1 = L[1], l2 = L[2];
                 L[6] += dt * (ck * l0 - sk * l1);
@@ -331,27 +339,33 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
                 L[10] += dt * L[4];
                 L[11] += dt * L[5];
             }
-            const int b0 = S.fb[i], b1 = S.fb[i + 1];
-            for (int bp = b0; bp < b1; ++bp) {
-                const int jp = S.lsm[bp] & 3;
+            const unsigned legs = (unsigned)(smask >> (4 * i)) & 15u;
+            int bp = __popcll(smask & ((1ull << (4 * i)) - 1ull));  // first stance leg-step of step i
 #pragma unroll
-                for (int ap = 0; ap < 3; ++ap) {
-                    const int cp = 3 * jp + ap;
-                    double val = 0.0;
-                    if constexpr (TERRAIN) {
+            for (int jp = 0; jp < 4; ++jp) {
+                if (!((legs >> jp) & 1u)) continue;  // uniform
+                if (i <= vkk) {
+                    const int vb0 = 16 * (bp / 5) + 3 * (bp % 5);  // first variable of leg-step bp
+                    const int tp = vb0 >> 4;
 #pragma unroll
-                        for (int q = 0; q < 6; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
-                    } else {  // flat ground: rows 3-5 of G0 are dt/m I (dense_prologue) -- the same sum, bit for bit
+                    for (int ap = 0; ap < 3; ++ap) {
+                        const int cp = 3 * jp + ap;
+                        double val = 0.0;
+                        if constexpr (TERRAIN) {
 #pragma unroll
-                        for (int q = 0; q < 3; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
-                        val = fma(dtm, L[9 + ap], val);
+                            for (int q = 0; q < 6; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+                        } else {  // flat ground: rows 3-5 of G0 are dt/m I (dense_prologue) -- the same sum, bit for bit
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+                            val = fma(dtm, L[9 + ap], val);
+                        }
+                        if (bp == vb) val += rbl[ap];
+                        const int vp = vb0 + ap;
+                        if (tp <= vt) S.Ht[tix(tp, vt) * DN_TILE + toff(vp & 15, vw)] = val;
+                        if (tp == vt && i < vkk) S.Ht[tix(vt, vt) * DN_TILE + toff(vw, vp & 15)] = val;
                     }
-                    if (bp == vb) val += rbl[ap];
-                    const int vp = vidx(bp, ap);
-                    const int tp = vp >> 4;
-                    if (tp <= vt) S.Ht[tix(tp, vt) * DN_TILE + toff(vp & 15, vw)] = val;
-                    if (tp == vt && i < vk) S.Ht[tix(vt, vt) * DN_TILE + toff(vw, vp & 15)] = val;
                 }
+                ++bp;
             }
         }
     }

@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(64) lmpc_gi_kernel(const DevParams prm, const 
     GSTAMP_DECL
 
     const int rank = dense_prologue<TERRAIN>(prm, S, rec, normals, qp, H, smask, stl, lane);
-    dense_condense<TERRAIN>(prm, S, H, nls, lane);
+    dense_condense<TERRAIN>(prm, S, H, nls, smask, lane);
     GSTAMP(0);  // prologue + condensation
 
     const int lc = lane & 15, lr = lane >> 4;
