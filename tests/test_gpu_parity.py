@@ -427,6 +427,22 @@ def test_dense_path_edge_cases(mode, monkeypatch):
     assert np.all(g[2] == 0.0)
 
 
+def test_multiround_polish_vs_oracle(monkeypatch):
+    """A polish round that follows a polish round re-factors only from the tile of the first leg-step whose active set
+    changed; the diagonal-tile factors ahead of it are reused (lmpc_dense.hip, keep_tiles).  Every QP of a config-2
+    batch that needed two or more polish rounds matches the oracle, and some needed three."""
+    monkeypatch.delenv("LMPC_DENSE", raising=False)
+    p, H, rec, con = synth.config_batch(2, count=1024)
+    s = BatchedConvexQPSolver(p, H, max_batch=1024, dense_path="ipm")
+    g, st, it = s.solve(rec, con)
+    rounds = it >> 16
+    multi = np.nonzero(rounds >= 2)[0]
+    assert len(multi) >= 16 and np.any(rounds >= 3)
+    ref, _, _ = O.solve_batch(O.params_from(p), H, rec[multi], con[multi], n_threads=8)
+    assert np.all(st[multi] == 0)
+    assert rel_err(g[multi], ref) <= TOL_REGRESS
+
+
 def test_dense_path_api(monkeypatch):
     """lmpc_set_dense_path selects the dense kernel per context (ABI 3); the environment overrides it;
     H > 16 has no dense path; all paths give the same optimum."""
