@@ -39,7 +39,28 @@ def parse():
     ap.add_argument("--flat", action="store_true", help="config 4 without its terrain normals (reference problem)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
+    ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
+                    help="dense-path kernel (lmpc_set_dense_path); default: gi for config 4, ipm otherwise")
     return ap.parse_args()
+
+
+def host_cores():
+    """Host CPUs this process may run on: the affinity set, bounded by the cgroup CPU quota when one is set
+    (os.cpu_count() reports every CPU of the machine, also those a container's quota does not grant)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = total
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        quota = None
+    usable = min(aff, quota) if quota else aff
+    return usable, {"os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota}
 
 
 def kernel_label(mode):
@@ -100,9 +121,9 @@ def main():
     # Dense-path kernel per workload (fixed per context, so no answer depends on it): the interior point when every
     # SIMD holds about one QP and the launch waits for the slowest (configs 2/3/5), the dual active set -- half the
     # mean cost, a longer tail -- when each SIMD streams through many QPs (config 4: 64 per SIMD); DESIGN.md 4b.
-    # LMPC_DENSE, when set, overrides it.
-    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank,
-                                   dense_path="gi" if args.config == 4 else "ipm")
+    # --dense overrides it.
+    dense = args.dense or ("gi" if args.config == 4 else "ipm")
+    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank, dense_path=dense)
     seed = synth.BASE_SEED + args.config
     d_cmd = solver.synth_commands_device(synth.config_cfg(args.config), B, seed, first_index=first, device=dev)
     d_nrm = solver.synth_normals_device(B, seed, first_index=first, device=dev) if terrain else None
@@ -166,7 +187,7 @@ def main():
     grf = d_grf.cpu().numpy()
     st = d_st.cpu().numpy()
     it = d_it.cpu().numpy()
-    mode = solver.dense_path  # "ipm" (default), "gi" or "off" (H > 16, or LMPC_DENSE=0)
+    mode = solver.dense_path  # "ipm" (default), "gi" or "off" (H > 16, or --dense off)
     ipm_mean = float(np.mean(it & 0xFFFF))
     pol_mean = float(np.mean(it >> 16))
     if mode == "gi":  # iteration word = active-set steps | drops << 16 on the dense QPs
@@ -189,7 +210,7 @@ def main():
     op = O.params_from(p)
     nrm_all = None if d_nrm is None else d_nrm.cpu().numpy()
     rec_all, con_all = d_rec.cpu().numpy(), d_con.cpu().numpy()  # the very instances the GPU solved
-    cores = min(16, os.cpu_count() or 1)
+    cores, cpu_info = host_cores()  # every host CPU this process may use (count stated in the line)
     if world == 1 and not args.no_cpu:
         idx = np.arange(B)  # N = 1: every QP of the batch
     else:
@@ -218,17 +239,33 @@ def main():
             "kind": "port",
             "sample": f"{reps} x the rank-0 batch ({B} QPs, {wl_name}), fp64 dense Goldfarb-Idnani "
                       f"oracle over {cores} host threads, {ct:.1f} s wall",
+            "host": cpu_info,
         }
 
-    # HBM bytes per launch of this workload from the committed PMC pass (rocprofv3 FETCH_SIZE + WRITE_SIZE)
+    # HBM bytes per launch of this workload from the committed PMC pass (rocprofv3 FETCH_SIZE + WRITE_SIZE),
+    # and the fp64 flops the kernels really executed (SQ_INSTS_VALU_FLOPS_FP64 + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64)
     traffic_bytes = None
+    executed = None
+    wl = (wl_name if mode == ("gi" if args.config == 4 else "ipm") else f"{wl_name}/{mode}") if args.batch is None else None
     try:
         tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-        wl = wl_name if args.batch is None else None
         if wl in tr:
             traffic_bytes = tr[wl]["bytes_per_qp"] * B  # this rank's launch (config 4 at N > 1: 65536/N QPs)
     except (OSError, ValueError, KeyError):
         traffic_bytes = None
+    try:
+        fl = json.load(open(os.path.join(ROOT, "profiles", "pmc_flops.json")))
+        if wl in fl:
+            e = fl[wl]["flop_per_qp"]
+            executed = {
+                "flop_per_qp": e,
+                "achieved": e * B / (kernel_ms * 1e-3) / 1e12,
+                "frac": e * B / (kernel_ms * 1e-3) / 1e12 / roofline.FP64_PEAK_TFLOPS,
+                "valu_share": fl[wl]["valu_flop_per_qp"] / e,
+                "source": fl[wl]["source"],
+            }
+    except (OSError, ValueError, KeyError, ZeroDivisionError):
+        executed = None
 
     if rank == 0:
         line = {
@@ -255,7 +292,9 @@ def main():
                 "parallelism": f"dp{world} (independent QP shards, no collective)",
             },
             "roofline": {
-                "bound": "mfma",
+                # fp64 compute, not HBM; the counters show fp64 VALU work issued by a latency-bound wave (one
+                # QP per SIMD), not matrix-core throughput; the fp64 peak is the same for both
+                "bound": "fp64-valu-latency",
                 "achieved": achieved_tf,
                 "peak": roofline.FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
@@ -266,6 +305,7 @@ def main():
                 "flop_per_qp": flop_per_qp,
                 "flop_model": flop_model,
                 "riccati_flop_per_qp": riccati_flop_per_qp,
+                "executed": executed,
                 "hbm_gbs": roofline.qp_bytes(H) * B / (kernel_ms * 1e-3) / 1e9,
             },
             "cpu_baseline": cpu,

@@ -142,8 +142,15 @@ private:
         dims.num_levels = (int32_t)chain.size();
         if (dims.num_levels > LMPC_HOQP_MAX_LEVELS) throw std::invalid_argument("HoQp: too many levels");
         for (size_t l = 0; l < chain.size(); ++l) {
-            dims.eq_rows[l] = (int32_t)chain[l]->a_.rows();
-            dims.ineq_rows[l] = (int32_t)chain[l]->d_.rows();
+            const Task& t = *chain[l];
+            // every level's blocks have the first task's column count (HoQp.cpp:49), as hoqp.dims_of checks
+            if ((t.a_.rows() > 0 && t.a_.cols() != dims.num_vars) || (t.d_.rows() > 0 && t.d_.cols() != dims.num_vars))
+                throw std::invalid_argument("HoQp: level " + std::to_string(l) + " has a column count other than " +
+                                            std::to_string(dims.num_vars));
+            if (t.b_.size() != t.a_.rows() || t.f_.size() != t.d_.rows())
+                throw std::invalid_argument("HoQp: level " + std::to_string(l) + ": a/b or d/f row counts differ");
+            dims.eq_rows[l] = (int32_t)t.a_.rows();
+            dims.ineq_rows[l] = (int32_t)t.d_.rows();
         }
         const int64_t len = lmpc_hoqp_record_len(&dims);
         if (len < 0) throw std::invalid_argument("HoQp: dimensions outside lmpc_hoqp.h's limits");
@@ -161,7 +168,14 @@ private:
         const int S = lmpc_hoqp_slack_len(&dims);
         std::vector<double> x((size_t)(dims.num_levels * n)), w((size_t)(S > 0 ? S : 1));
         int32_t st = 0;
-        const int rc = lmpc_hoqp_solve_batch(context(dims), rec.data(), 1, x.data(), w.data(), &st, nullptr);
+        Slot& slot = context(dims);
+        int rc;
+        {
+            // a context's staging buffers and event are not thread-safe (lmpc_hoqp.h): same-shaped chains built
+            // on several threads take turns on the shared context for the whole pack/solve/copy-out
+            std::lock_guard<std::mutex> g(slot.mu);
+            rc = lmpc_hoqp_solve_batch(slot.ctx, rec.data(), 1, x.data(), w.data(), &st, nullptr);
+        }
         if (rc != LMPC_OK) throw std::runtime_error(std::string("lmpc_hoqp_solve_batch: ") + lmpc_strerror(rc));
         status_ = st;
         const size_t last = chain.size() - 1;
@@ -174,11 +188,15 @@ private:
     }
 
     // one device context per distinct shape, kept for the life of the process (the reference re-creates its
-    // QProblem per call); deliberately never destroyed: a static destructor would call into the HIP runtime
-    // during its own teardown
-    static lmpc_hoqp_ctx* context(const lmpc_hoqp_dims& d) {
+    // QProblem per call), with the mutex its users take turns on; deliberately never destroyed: a static
+    // destructor would call into the HIP runtime during its own teardown
+    struct Slot {
+        lmpc_hoqp_ctx* ctx = nullptr;
+        std::mutex mu;
+    };
+    static Slot& context(const lmpc_hoqp_dims& d) {
         static std::mutex mu;
-        static std::map<std::vector<int32_t>, lmpc_hoqp_ctx*> ctxs;
+        static std::map<std::vector<int32_t>, Slot*> ctxs;
         std::vector<int32_t> key{d.num_vars, d.num_levels};
         for (int l = 0; l < LMPC_HOQP_MAX_LEVELS; ++l) {
             key.push_back(d.eq_rows[l]);
@@ -186,12 +204,14 @@ private:
         }
         std::lock_guard<std::mutex> g(mu);
         auto it = ctxs.find(key);
-        if (it != ctxs.end()) return it->second;
+        if (it != ctxs.end()) return *it->second;
         lmpc_hoqp_ctx* c = nullptr;
         const int rc = lmpc_hoqp_create(&d, 1, 0, &c);
         if (rc != LMPC_OK) throw std::runtime_error(std::string("lmpc_hoqp_create: ") + lmpc_strerror(rc));
-        ctxs.emplace(key, c);
-        return c;
+        Slot* slot = new Slot();
+        slot->ctx = c;
+        ctxs.emplace(key, slot);
+        return *slot;
     }
 
     Task task_, stacked_tasks_;

@@ -49,8 +49,9 @@
 extern "C" {
 #endif
 
-#define LMPC_ABI_VERSION 4 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
-                              4: warm start (lmpc_solve_batch_warm, lmpc_shift_active_set) */
+#define LMPC_ABI_VERSION 5 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
+                              4: warm start (lmpc_solve_batch_warm, lmpc_shift_active_set);
+                              5: dense-path caps in lmpc_options, no environment overrides */
 #define LMPC_MAX_HORIZON 32
 
 /* return codes (API level) */
@@ -96,6 +97,12 @@ typedef struct lmpc_options {
     double tol_mu;    /* IPM stop: mean complementarity (default 1e-8) */
     double tol_p;     /* polish primal feasibility, relative to f_max (default 1e-9) */
     double tol_d;     /* polish multiplier sign, relative to gradient scale (default 1e-9) */
+    /* ABI 5: the dense paths' caps and the warm-start budget (were environment hooks).  None of them
+     * changes the answer: a QP a dense kernel leaves is solved by the Riccati kernel in the same call. */
+    int gi_max_steps;      /* dual active set: steps before the hand-over (default 240) */
+    int dense_iter_cap;    /* condensed interior point: iterations before the hand-over (default 0 = none) */
+    int dense_polish_iter; /* condensed interior point: first-attempt iterations before the polish (default 40) */
+    int warm_rounds;       /* warm start: polish rounds before the cold fallback (default 12) */
 } lmpc_options;
 
 /* Robot presets: gazebo_go1_convex.yaml:39-71 (+ LeggedState.cpp:146,155-160
@@ -125,7 +132,7 @@ int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
  * LMPC_DENSE_OFF sends every QP to the Riccati kernel.  All return the same optimum: a dense QP left
  * without a verified optimum (iteration or step cap, non-finite iterate) is solved by the Riccati
  * kernel in the same call, so its status is the Riccati kernel's.  Set it before
- * solving; the environment variable LMPC_DENSE (0 / ipm / gi), when set, overrides this call.
+ * solving; no environment variable changes it (ABI 5).
  * lmpc_get_dense_path returns the path in effect (LMPC_DENSE_OFF when H > 16). */
 #define LMPC_DENSE_OFF 0
 #define LMPC_DENSE_IPM 1

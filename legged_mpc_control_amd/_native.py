@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     # ABI 3: dense-path selection
     "lmpc_set_dense_path", "lmpc_get_dense_path",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 # include/lmpc/lmpc_hoqp.h: batched hierarchical QP (whole-body control)
 HOQP_SYMBOLS = (
     "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
@@ -67,6 +67,11 @@ class LmpcOptions(ctypes.Structure):
         ("tol_mu", ctypes.c_double),
         ("tol_p", ctypes.c_double),
         ("tol_d", ctypes.c_double),
+        # ABI 5: the dense paths' caps and the warm-start budget
+        ("gi_max_steps", ctypes.c_int),
+        ("dense_iter_cap", ctypes.c_int),
+        ("dense_polish_iter", ctypes.c_int),
+        ("warm_rounds", ctypes.c_int),
     ]
 
 

@@ -47,7 +47,6 @@ struct lmpc_ctx {
     uint8_t* h_out = nullptr;
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
     uint8_t* d_done = nullptr;    // per-QP flag: solved by the dense-path kernel (else the Riccati kernel solves it)
-    bool dense_env = false;       // LMPC_DENSE set: it overrides lmpc_set_dense_path
     size_t scratch_qps = 0;
     double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
     uint8_t* d_ccon = nullptr;
@@ -82,6 +81,10 @@ void fill_options(lmpc::DevParams& d, const lmpc_options* o) {
     d.tol_mu = o->tol_mu;
     d.tol_p = o->tol_p;
     d.tol_d = o->tol_d;
+    d.gi_max_steps = o->gi_max_steps;
+    d.dense_iter_cap = o->dense_iter_cap > 0 ? o->dense_iter_cap : (1 << 30);  // 0: never hand over
+    d.dense_polish_iter = o->dense_polish_iter;
+    d.warm_rounds = o->warm_rounds;
 }
 
 bool params_ok(const lmpc_params* p) {
@@ -180,22 +183,10 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
     fill_options(c->prm, &o);
     c->prm.H = horizon;
     // condensed dense path for H <= DENSE_MAX_H: the interior point (lmpc_dense.hip) by default;
-    // LMPC_DENSE=gi selects the dual active set (lmpc_gi.hip), LMPC_DENSE=0 the Riccati kernel for every
-    // QP (A/B checks).  The choice is fixed per context, never per launch, so a QP's answer does not
-    // depend on the batch it is solved in.  Why the interior point is the default: DESIGN.md 4b.
-    const char* dn = std::getenv("LMPC_DENSE");
-    c->dense_env = dn && dn[0];
-    c->prm.dense = horizon > lmpc::DENSE_MAX_H || (dn && dn[0] == '0') ? 0 : (dn && dn[0] == 'g') ? 2 : 1;
-    {
-        const char* gm = std::getenv("LMPC_GI_MAX_STEPS");  // test hook: exercise the hand-over to the Riccati kernel
-        c->prm.gi_max_steps = gm ? std::atoi(gm) : 240;
-        const char* dc = std::getenv("LMPC_DENSE_ITER_CAP");  // test hook: the interior point's hand-over
-        c->prm.dense_iter_cap = dc ? std::atoi(dc) : (1 << 30);
-        const char* dp = std::getenv("LMPC_DENSE_POLISH_ITER");  // tuning hook (tools/)
-        c->prm.dense_polish_iter = dp ? std::atoi(dp) : LMPC_DENSE_POLISH_ITER;
-        const char* wr = std::getenv("LMPC_WARM_ROUNDS");  // tuning hook (tools/)
-        c->prm.warm_rounds = wr ? std::atoi(wr) : 12;  // tools/tick_latency sweep: 4 -> 0.59 ms, 12 -> 0.35 ms at H=30
-    }
+    // lmpc_set_dense_path selects the dual active set (lmpc_gi.hip) or the Riccati kernel for every QP.
+    // The choice is fixed per context, never per launch, so a QP's answer does not depend on the batch it
+    // is solved in.  Why the interior point is the default: DESIGN.md 4b.
+    c->prm.dense = horizon > lmpc::DENSE_MAX_H ? 0 : 1;
     if (hipDeviceGetAttribute(&c->prm.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         c->prm.cus = 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -244,7 +235,8 @@ void lmpc_destroy(lmpc_ctx* c) {
 
 int lmpc_set_options(lmpc_ctx* c, const lmpc_options* o) {
     if (!c || !o || o->max_iter < 1 || o->max_rounds < 1 || o->max_attempts < 1 || !(o->tol_mu > 0.0) ||
-        !(o->tol_p >= 0.0) || !(o->tol_d >= 0.0))
+        !(o->tol_p >= 0.0) || !(o->tol_d >= 0.0) || o->gi_max_steps < 1 || o->dense_iter_cap < 0 ||
+        o->dense_polish_iter < 1 || o->warm_rounds < 1)
         return LMPC_ERR_ARG;
     fill_options(c->prm, o);
     return LMPC_OK;
@@ -258,7 +250,7 @@ int lmpc_set_params(lmpc_ctx* c, const lmpc_params* p) {
 
 int lmpc_set_dense_path(lmpc_ctx* c, int path) {
     if (!c || path < LMPC_DENSE_OFF || path > LMPC_DENSE_GI) return LMPC_ERR_ARG;
-    if (!c->dense_env && c->H <= lmpc::DENSE_MAX_H) c->prm.dense = path;
+    if (c->H <= lmpc::DENSE_MAX_H) c->prm.dense = path;
     return LMPC_OK;
 }
 

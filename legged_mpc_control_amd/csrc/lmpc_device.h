@@ -27,7 +27,7 @@ struct DevParams {
     int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel
     int dense_polish_iter;  // condensed interior point: iterations of the first attempt before the active-set polish
     int dense_iter_cap;  // condensed interior point: IPM iterations after which a QP is handed to the Riccati
-                         // kernel (test hook LMPC_DENSE_ITER_CAP; default: never, max_iter governs)
+                         // kernel (lmpc_options.dense_iter_cap; default: never, max_iter governs)
     int cus;           // compute units of the device (launch shaping only)
     // warm start of the Riccati kernel (per QP and leg-step [B][H][4]: bits 0-4 = active pyramid faces and
     // bound, 15 = lift-off apex).  warm_act != nullptr: the kernel starts in the active-set polish from it and
@@ -37,9 +37,6 @@ struct DevParams {
     uint8_t* act_out;
     int warm_rounds;   // polish rounds a warm start may take before the cold fallback
 };
-#ifndef LMPC_DENSE_POLISH_ITER
-#define LMPC_DENSE_POLISH_ITER 40  // = lmpc_options_default max_iter: the polish only once the IPM has converged
-#endif
 constexpr int DENSE_MAX_LS = 20;  // 5 leg-steps per 16-wide tile x 4 tiles (lmpc_dense.hip)
 constexpr int DENSE_MAX_H = 16;   // the dense path's per-step LDS arrays
 

@@ -48,6 +48,10 @@ void lmpc_options_default(lmpc_options* o) {
     o->tol_mu = 1e-8;
     o->tol_p = 1e-9;
     o->tol_d = 1e-9;
+    o->gi_max_steps = 240;
+    o->dense_iter_cap = 0;
+    o->dense_polish_iter = 40;  // = max_iter: the polish only once the interior point has converged
+    o->warm_rounds = 12;        // tools/tick_latency sweep: 4 -> 0.59 ms, 12 -> 0.35 ms per tick at H = 30
 }
 
 int lmpc_record_len(int horizon) { return 33 + 12 * horizon; }

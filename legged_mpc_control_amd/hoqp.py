@@ -15,6 +15,7 @@ GPU these raise.  Numerics and what is comparable across solvers: include/lmpc/l
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -108,6 +109,9 @@ class HoqpBatch:
         self.rec_len = record_len(dims)
         self.slack_len = int(self._L.lmpc_hoqp_slack_len(ctypes.byref(dims)))
         self._ctx = ctypes.c_void_p()
+        # a context is not thread-safe (lmpc_hoqp.h) and ctypes releases the GIL during a call: every call that
+        # uses it (staging buffers, stream, event) holds this lock
+        self._lock = threading.Lock()
         N.check(self._L.lmpc_hoqp_create(ctypes.byref(dims), max_batch, device, ctypes.byref(self._ctx)),
                 "lmpc_hoqp_create")
 
@@ -131,7 +135,8 @@ class HoqpBatch:
             o.tol_mu = tol_mu
         if tol_res is not None:
             o.tol_res = tol_res
-        N.check(self._L.lmpc_hoqp_set_options(self._ctx, ctypes.byref(o)), "lmpc_hoqp_set_options")
+        with self._lock:
+            N.check(self._L.lmpc_hoqp_set_options(self._ctx, ctypes.byref(o)), "lmpc_hoqp_set_options")
 
     def solve(self, records: np.ndarray):
         """Host path.  records [B][rec_len] -> x [B][levels][n], slack [B][total ineq rows], status [B],
@@ -143,9 +148,10 @@ class HoqpBatch:
         st = np.zeros(B, dtype=np.int32)
         it = np.zeros((B, self.levels), dtype=np.int32)
         dp, i32p = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
-        N.check(self._L.lmpc_hoqp_solve_batch(self._ctx, rec.ctypes.data_as(dp), B, x.ctypes.data_as(dp),
-                                              w.ctypes.data_as(dp), st.ctypes.data_as(i32p),
-                                              it.ctypes.data_as(i32p)), "lmpc_hoqp_solve_batch")
+        with self._lock:
+            N.check(self._L.lmpc_hoqp_solve_batch(self._ctx, rec.ctypes.data_as(dp), B, x.ctypes.data_as(dp),
+                                                  w.ctypes.data_as(dp), st.ctypes.data_as(i32p),
+                                                  it.ctypes.data_as(i32p)), "lmpc_hoqp_solve_batch")
         return x, w[:, :self.slack_len], st, it
 
     def solve_device(self, d_rec, d_x, d_w, d_status=None, d_iters=None, stream=None):
@@ -153,21 +159,47 @@ class HoqpBatch:
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        B = d_rec.shape[0]
+        B = int(d_rec.shape[0]) if d_rec.dim() >= 1 else -1
+        dev = torch.device("cuda", self.device)
+        check_device_tensor("d_rec", d_rec, torch.float64, (B, self.rec_len), dev)
+        check_device_tensor("d_x", d_x, torch.float64, (B, self.levels, self.n), dev)
+        check_device_tensor("d_w", d_w, torch.float64, (B, max(self.slack_len, 1)), dev, allow_shape=(B, self.slack_len))
+        if d_status is not None:
+            check_device_tensor("d_status", d_status, torch.int32, (B,), dev)
+        if d_iters is not None:
+            check_device_tensor("d_iters", d_iters, torch.int32, (B, self.levels), dev)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-        N.check(self._L.lmpc_hoqp_solve_device(self._ctx, ptr(d_rec), B, ptr(d_x), ptr(d_w), ptr(d_status),
-                                               ptr(d_iters), ctypes.c_void_p(s.cuda_stream)),
-                "lmpc_hoqp_solve_device")
+        with self._lock:
+            N.check(self._L.lmpc_hoqp_solve_device(self._ctx, ptr(d_rec), B, ptr(d_x), ptr(d_w), ptr(d_status),
+                                                   ptr(d_iters), ctypes.c_void_p(s.cuda_stream)),
+                    "lmpc_hoqp_solve_device")
+
+
+def check_device_tensor(name, t, dtype, shape, device, allow_shape=None):
+    """A raw pointer handed to the device path must be a contiguous tensor of this dtype and shape on the
+    context's device: anything else turns into out-of-bounds device writes or wrong results."""
+    if t is None or not hasattr(t, "is_cuda") or not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor")
+    if t.device != device:
+        raise ValueError(f"{name}: on {t.device}, the context is on {device}")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if tuple(t.shape) != tuple(shape) and (allow_shape is None or tuple(t.shape) != tuple(allow_shape)):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
 
 
 _batches = {}
+_batches_lock = threading.Lock()
 
 
 def _batch_for(dims: N.LmpcHoqpDims, device: int) -> HoqpBatch:
     key = (dims.num_vars, dims.num_levels, tuple(dims.eq_rows), tuple(dims.ineq_rows), device)
-    if key not in _batches:
-        _batches[key] = HoqpBatch(dims, 1, device)
-    return _batches[key]
+    with _batches_lock:
+        if key not in _batches:
+            _batches[key] = HoqpBatch(dims, 1, device)
+        return _batches[key]
 
 
 class HoQp:

@@ -49,6 +49,17 @@ def grf_to_torque(kin: N.LmpcLegKin, rot, joint_pos, grf0) -> np.ndarray:
     return tau
 
 
+def solver_options(**overrides) -> N.LmpcOptions:
+    """lmpc_options_default with the named fields replaced, e.g. solver_options(gi_max_steps=20)."""
+    o = N.LmpcOptions()
+    N.lib().lmpc_options_default(ctypes.byref(o))
+    for k, v in overrides.items():
+        if not hasattr(o, k):
+            raise AttributeError(f"lmpc_options has no field {k!r}")
+        setattr(o, k, v)
+    return o
+
+
 class BatchedConvexQPSolver:
     """A device context: horizon H, host staging for up to max_batch QPs."""
 
@@ -56,7 +67,7 @@ class BatchedConvexQPSolver:
 
     def __init__(self, params: N.LmpcParams, horizon: int, max_batch: int = 1, device: int = 0,
                  options: N.LmpcOptions | None = None, dense_path: str | None = None):
-        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path; LMPC_DENSE overrides it)."""
+        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path)."""
         if not (1 <= horizon <= N.LMPC_MAX_HORIZON):
             raise ValueError(f"horizon must be in [1, {N.LMPC_MAX_HORIZON}]")
         self._L = N.lib()

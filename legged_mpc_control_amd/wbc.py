@@ -22,6 +22,8 @@ import numpy as np
 
 from .hoqp import Task
 
+WBC_RECORD_LEN = 4472  # doubles per WBC chain record (lmpc_hoqp_record_len of lmpc_hoqp_dims_wbc)
+
 NQ = 18            # generalized coordinates (6 base + 12 joints)
 NF = 12            # 4 three-dof contacts
 NTAU = 12          # actuated joints
@@ -178,7 +180,7 @@ def record_native(inp) -> np.ndarray:
 
     from ._native import check, lib
 
-    rec = np.zeros(4472)
+    rec = np.zeros(WBC_RECORD_LEN)
     check(lib().lmpc_wbc_tasks(ctypes.byref(inp), rec.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
           "lmpc_wbc_tasks")
     return rec
@@ -191,9 +193,14 @@ def records_device(d_inputs, d_records, stream=None):
 
     import torch
 
-    from ._native import check, lib
+    from ._native import LmpcWbcInput, check, lib
+    from .hoqp import check_device_tensor
 
     s = stream if stream is not None else torch.cuda.current_stream()
+    B = int(d_inputs.shape[0]) if d_inputs.dim() >= 1 else -1
+    dev = d_inputs.device if getattr(d_inputs, "is_cuda", False) else torch.device("cuda", torch.cuda.current_device())
+    check_device_tensor("d_inputs", d_inputs, torch.uint8, (B, ctypes.sizeof(LmpcWbcInput)), dev)
+    check_device_tensor("d_records", d_records, torch.float64, (B, WBC_RECORD_LEN), dev)
     check(lib().lmpc_wbc_tasks_device(ctypes.c_void_p(d_inputs.data_ptr()), d_inputs.shape[0],
                                       ctypes.c_void_p(d_records.data_ptr()), ctypes.c_void_p(s.cuda_stream)),
           "lmpc_wbc_tasks_device")

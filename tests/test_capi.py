@@ -38,7 +38,7 @@ def test_exports_are_c_linkage():
 
 def test_abi_and_strings():
     lib = N.lib()
-    assert lib.lmpc_abi_version() == 4
+    assert lib.lmpc_abi_version() == 5
     assert lib.lmpc_record_len(10) == 153 and lib.lmpc_record_len(30) == 393
     assert lib.lmpc_strerror(0) == b"ok"
     assert lib.lmpc_strerror(-1) == b"invalid argument"
@@ -46,7 +46,7 @@ def test_abi_and_strings():
 
 def test_struct_layouts():
     assert ctypes.sizeof(N.LmpcParams) == 8 * (12 + 12 + 1 + 9 + 4)
-    assert ctypes.sizeof(N.LmpcOptions) == 4 * 3 + 4 + 8 * 3  # 3 ints + pad + 3 doubles
+    assert ctypes.sizeof(N.LmpcOptions) == 4 * 3 + 4 + 8 * 3 + 4 * 4  # 3 ints + pad + 3 doubles + 4 ints (ABI 5)
     assert ctypes.sizeof(N.LmpcStateIn) == 8 * (3 * 4 + 9 + 12 + 3 * 4)
     assert ctypes.sizeof(N.LmpcCommand) == N.COMMAND_BYTES == 384  # static_assert'ed in lmpc_common.h
     assert N.LmpcCommand.gait.offset == 376 and N.LmpcCommand.plan_contacts.offset == 380
@@ -97,3 +97,21 @@ def test_no_oracle_in_product_path():
                 assert not re.search(r"^\s*(from|import)\s+oracle|lmpc_oracle|liblmpc_oracle", txt, re.M), f
     out = subprocess.run(["ldd", N.LIB_PATH], capture_output=True, text=True).stdout
     assert "oracle" not in out
+
+
+def test_options_defaults_and_no_environment_overrides():
+    """ABI 5: the dense paths' caps and the warm-start budget are lmpc_options fields with documented defaults,
+    and no product source reads the environment (a stray variable in a ROS process must not change
+    the algorithm)."""
+    from legged_mpc_control_amd import solver_options
+
+    o = solver_options()
+    assert (o.max_iter, o.max_rounds, o.max_attempts) == (40, 4, 3)
+    assert (o.gi_max_steps, o.dense_iter_cap, o.dense_polish_iter, o.warm_rounds) == (240, 0, 40, 12)
+    assert solver_options(gi_max_steps=20).gi_max_steps == 20
+    with pytest.raises(AttributeError):
+        solver_options(no_such_field=1)
+    csrc = os.path.join(ROOT, "legged_mpc_control_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".cpp", ".hip", ".h")):
+            assert "getenv" not in open(os.path.join(csrc, f)).read(), f

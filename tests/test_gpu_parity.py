@@ -16,13 +16,14 @@ import pytest
 
 from conftest import ROOT, golden_files, lmpc_params_from, load_golden, rel_err
 
-from legged_mpc_control_amd import BatchedConvexQPSolver, synth
+from legged_mpc_control_amd import BatchedConvexQPSolver, solver_options, synth
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4          # north-star parity bar
 TOL_REGRESS = 1e-7  # regression guard
+DENSE = {"ipm": "ipm", "gi": "gi", "0": "off"}  # test ids -> lmpc_set_dense_path
 
 
 def feasibility_violation(grf, con, mu=0.3, fmax=180.0):
@@ -44,13 +45,13 @@ def torch_dev():
 
 @pytest.mark.parametrize("mode", ["ipm", "gi", "0"])
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: os.path.basename(p))
-def test_golden_fixtures(path, mode, monkeypatch):
+def test_golden_fixtures(path, mode):
     """Every certified golden instance on each device path: the condensed interior point (default),
     the condensed dual active set and the Riccati kernel (QPs the dense kernels do not take -- more
     than 20 stance leg-steps, H > 16, all-swing -- run on the Riccati kernel in every mode)."""
-    monkeypatch.setenv("LMPC_DENSE", mode)
     g = load_golden(path)
-    s = BatchedConvexQPSolver(lmpc_params_from(g["params"]), g["H"], max_batch=g["rec"].shape[0])
+    s = BatchedConvexQPSolver(lmpc_params_from(g["params"]), g["H"], max_batch=g["rec"].shape[0],
+                              dense_path=DENSE[mode])
     grf, status, iters = s.solve(g["rec"], g["contact"], normals=g["normals"])
     assert np.all(status == 0), status
     err = rel_err(grf, g["grf"])
@@ -81,18 +82,16 @@ def test_full_config2_batch_vs_oracle():
 
 
 @pytest.mark.parametrize("cid,mode", [(3, "ipm"), (4, "ipm"), (4, "gi"), (5, "ipm")])
-def test_full_size_properties(cid, mode, torch_dev, monkeypatch):
+def test_full_size_properties(cid, mode, torch_dev):
     """Configs 3/4/5 at full batch: converged, feasible, swing legs exactly zero,
     bitwise deterministic, permutation-invariant and shard-invariant, including a shard small enough
     to change the Riccati kernel instance (config 4 also with the dual active-set kernel on its
     dense-eligible QPs)."""
     import torch
 
-    monkeypatch.setenv("LMPC_DENSE", mode)
-
     p, H, rec, con = synth.config_batch(cid)
     B = rec.shape[0]
-    s = BatchedConvexQPSolver(p, H, max_batch=0)
+    s = BatchedConvexQPSolver(p, H, max_batch=0, dense_path=mode)
     d_rec, d_con = torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev)
     out = torch.empty((B, H, 12), dtype=torch.float64, device=torch_dev)
     st = torch.empty(B, dtype=torch.int32, device=torch_dev)
@@ -160,13 +159,12 @@ def test_horizon_range(H):
 
 
 @pytest.mark.parametrize("H,mode", [(16, "0"), (16, "ipm"), (12, "gi"), (17, "ipm")])
-def test_riccati_instances_large_batch(H, mode, monkeypatch):
+def test_riccati_instances_large_batch(H, mode):
     """Batches above one QP per SIMD (2048 mixed-gait QPs): at H <= 16 the Riccati kernel runs its two-wave
     instance, at H = 17 the one-wave two-leg-step instance.  Sampled QPs vs the oracle, and a 256-QP shard
     (one-wave instance) bit-identical to the same QPs inside the large batch."""
-    monkeypatch.setenv("LMPC_DENSE", mode)
     p, _, rec, con = synth.config_batch(4, count=2048, first_index=4242, H=H)
-    s = BatchedConvexQPSolver(p, H, max_batch=2048)
+    s = BatchedConvexQPSolver(p, H, max_batch=2048, dense_path=DENSE[mode])
     grf, status, _ = s.solve(rec, con)
     assert np.all(status == 0), np.bincount(status)
     viol, swing_nonzero = feasibility_violation(grf, con, p.mu, p.f_max)
@@ -269,16 +267,15 @@ def test_cpp_dropin_program_vs_oracle():
 
 
 @pytest.mark.parametrize("mode", ["ipm", "0"])
-def test_solve_options_and_status_codes(mode, monkeypatch):
+def test_solve_options_and_status_codes(mode):
     """IPM options (max_iter / attempts) on the two interior-point paths: the condensed dense kernel
-    (LMPC_DENSE=ipm) and the Riccati kernel (LMPC_DENSE=0).  The dual active-set kernel has no
+    (dense path "ipm") and the Riccati kernel (dense path "off").  The dual active-set kernel has no
     interior-point iterations; its step cap hands a QP to the Riccati kernel."""
     from legged_mpc_control_amd import LmpcOptions
     from legged_mpc_control_amd import _native as N
 
-    monkeypatch.setenv("LMPC_DENSE", mode)
     p, H, rec, con = synth.config_batch(2, count=32)
-    s = BatchedConvexQPSolver(p, H, max_batch=32)
+    s = BatchedConvexQPSolver(p, H, max_batch=32, dense_path=DENSE[mode])
     o = LmpcOptions()
     N.lib().lmpc_options_default(o)
     o.max_iter, o.max_attempts = 2, 1  # far too few IPM iterations: polish may not verify
@@ -379,19 +376,17 @@ def test_terrain_rejects_bad_normals():
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("mode", ["ipm", "gi"])
 @pytest.mark.parametrize("cid", [2, 4])
-def test_dense_and_riccati_paths_agree(cid, mode, monkeypatch):
+def test_dense_and_riccati_paths_agree(cid, mode):
     """Every config-2 QP (and the trot-like config-4 QPs) runs on a condensed dense kernel -- the
-    interior point (LMPC_DENSE=ipm) or the dual active set (LMPC_DENSE=gi); with LMPC_DENSE=0 the
+    interior point ("ipm") or the dual active set ("gi"); with the dense path "off" the
     same QPs run on the Riccati path.  All must give the oracle's optimum."""
     p, H, rec, con = synth.config_batch(cid, count=512, first_index=777)
     nrm = synth.config_normals(cid, count=512, first_index=777)
     nls = con.sum((1, 2))
     dense = (nls >= 1) & (nls <= 20)
     assert np.any(dense) and (cid == 4 or np.all(dense))
-    monkeypatch.setenv("LMPC_DENSE", mode)
-    gd, sd, itd = BatchedConvexQPSolver(p, H, max_batch=512).solve(rec, con, normals=nrm)
-    monkeypatch.setenv("LMPC_DENSE", "0")
-    gr, sr, itr = BatchedConvexQPSolver(p, H, max_batch=512).solve(rec, con, normals=nrm)
+    gd, sd, itd = BatchedConvexQPSolver(p, H, max_batch=512, dense_path=mode).solve(rec, con, normals=nrm)
+    gr, sr, itr = BatchedConvexQPSolver(p, H, max_batch=512, dense_path="off").solve(rec, con, normals=nrm)
     ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8, normals=nrm)
     assert fails == 0 and np.all(sd == 0) and np.all(sr == 0)
     assert rel_err(gd, ref) <= TOL_REGRESS and rel_err(gr, ref) <= TOL_REGRESS
@@ -408,10 +403,9 @@ def test_dense_and_riccati_paths_agree(cid, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["ipm", "gi"])
-def test_dense_path_edge_cases(mode, monkeypatch):
+def test_dense_path_edge_cases(mode):
     """Dense-path QPs with fewer than 20 stance leg-steps (partly padded tiles), a single stance
     leg-step, and the all-swing QP (left to the Riccati kernel)."""
-    monkeypatch.setenv("LMPC_DENSE", mode)
     p, H, rec, con = synth.config_batch(2, count=8, first_index=31)
     con = con.copy()
     con[0, :, :] = 0; con[0, 0, 1] = 1          # one stance leg-step
@@ -419,7 +413,7 @@ def test_dense_path_edge_cases(mode, monkeypatch):
     con[2, :, :] = 0                            # all swing -> zeros (Riccati kernel)
     con[3, :, 0] = 1; con[3, :, 1:] = 0         # one leg in stance all horizon
     con[4, 0:4, :] = 1                          # 16 + ... stance: > 20 -> Riccati
-    s = BatchedConvexQPSolver(p, H, max_batch=8)
+    s = BatchedConvexQPSolver(p, H, max_batch=8, dense_path=mode)
     g, st, it = s.solve(rec, con)
     ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=4)
     assert fails == 0 and np.all(st == 0), st
@@ -427,11 +421,10 @@ def test_dense_path_edge_cases(mode, monkeypatch):
     assert np.all(g[2] == 0.0)
 
 
-def test_multiround_polish_vs_oracle(monkeypatch):
+def test_multiround_polish_vs_oracle():
     """A polish round that follows a polish round re-factors only from the tile of the first leg-step whose active set
     changed; the diagonal-tile factors ahead of it are reused (lmpc_dense.hip, keep_tiles).  Every QP of a config-2
     batch that needed two or more polish rounds matches the oracle, and some needed three."""
-    monkeypatch.delenv("LMPC_DENSE", raising=False)
     p, H, rec, con = synth.config_batch(2, count=1024)
     s = BatchedConvexQPSolver(p, H, max_batch=1024, dense_path="ipm")
     g, st, it = s.solve(rec, con)
@@ -444,9 +437,8 @@ def test_multiround_polish_vs_oracle(monkeypatch):
 
 
 def test_dense_path_api(monkeypatch):
-    """lmpc_set_dense_path selects the dense kernel per context (ABI 3); the environment overrides it;
-    H > 16 has no dense path; all paths give the same optimum."""
-    monkeypatch.delenv("LMPC_DENSE", raising=False)
+    """lmpc_set_dense_path selects the dense kernel per context (ABI 3); no environment variable changes it
+    (ABI 5); H > 16 has no dense path; all paths give the same optimum."""
     p, H, rec, con = synth.config_batch(2, count=64, first_index=9000)
     out = {}
     for path in ("ipm", "gi", "off"):
@@ -458,8 +450,9 @@ def test_dense_path_api(monkeypatch):
         assert np.all(st == 0) and rel_err(g, ref) <= TOL_REGRESS, path
     assert np.array_equal(out["ipm"][2], out["off"][2])                 # same Newton systems
     assert not np.array_equal(out["gi"][2], out["ipm"][2])              # active-set steps instead
-    monkeypatch.setenv("LMPC_DENSE", "0")
-    assert BatchedConvexQPSolver(p, H, max_batch=4, dense_path="gi").dense_path == "off"
+    monkeypatch.setenv("LMPC_DENSE", "0")  # the old override is gone: the explicit choice stands
+    assert BatchedConvexQPSolver(p, H, max_batch=4, dense_path="gi").dense_path == "gi"
+    assert BatchedConvexQPSolver(p, H, max_batch=4).dense_path == "ipm"
     monkeypatch.delenv("LMPC_DENSE")
     p30, H30, _, _ = synth.config_batch(5, count=1)
     assert BatchedConvexQPSolver(p30, H30, max_batch=1, dense_path="gi").dense_path == "off"
@@ -468,16 +461,15 @@ def test_dense_path_api(monkeypatch):
     assert ConvexQPSolver(p.q_weights, p.r_weights, horizon=10)._dev.dense_path == "gi"
 
 
-def test_gi_step_cap_hands_over_to_riccati(monkeypatch):
+def test_gi_step_cap_hands_over_to_riccati():
     """A dual active-set QP that reaches the step cap is solved by the Riccati kernel in the same
     launch: same optimum, and its iteration word carries the interior-point counts (polish rounds
     >= 1 in the high bits) instead of the active-set steps."""
     p, H, rec, con = synth.config_batch(2, count=256, first_index=4242)
-    monkeypatch.setenv("LMPC_DENSE", "gi")
-    monkeypatch.setenv("LMPC_GI_MAX_STEPS", "20")
-    g, st, it = BatchedConvexQPSolver(p, H, max_batch=256).solve(rec, con)
-    monkeypatch.setenv("LMPC_GI_MAX_STEPS", "1000")
-    g2, st2, it2 = BatchedConvexQPSolver(p, H, max_batch=256).solve(rec, con)
+    g, st, it = BatchedConvexQPSolver(p, H, max_batch=256, dense_path="gi",
+                                      options=solver_options(gi_max_steps=20)).solve(rec, con)
+    g2, st2, it2 = BatchedConvexQPSolver(p, H, max_batch=256, dense_path="gi",
+                                         options=solver_options(gi_max_steps=1000)).solve(rec, con)
     ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
     assert fails == 0 and np.all(st == 0) and np.all(st2 == 0)
     handed = (it2 & 0xFFFF) > 20
@@ -519,17 +511,17 @@ def test_warm_start(cid):
 
 
 @pytest.mark.parametrize("path", ["host", "device"])
-def test_ipm_iteration_cap_hands_over_to_riccati(path, torch_dev, monkeypatch):
+def test_ipm_iteration_cap_hands_over_to_riccati(path, torch_dev):
     """A condensed interior-point QP left without a verified optimum is solved by the Riccati kernel in the same
-    call, as the dual active set's are: with the dense kernel capped at 3 iterations (test hook
-    LMPC_DENSE_ITER_CAP) every config-2 QP is handed over, so the answer, status and iteration word are the
+    call, as the dual active set's are: with the dense kernel capped at 3 iterations
+    (lmpc_options.dense_iter_cap) every config-2 QP is handed over, so the answer, status and iteration word are the
     Riccati kernel's own, bit for bit."""
     import torch
 
     p, H, rec, con = synth.config_batch(2, count=256, first_index=606)
 
-    def run():
-        s = BatchedConvexQPSolver(p, H, max_batch=256)
+    def run(mode, cap=0):
+        s = BatchedConvexQPSolver(p, H, max_batch=256, dense_path=mode, options=solver_options(dense_iter_cap=cap))
         if path == "host":
             return s.solve(rec, con)
         out = torch.empty((256, H, 12), dtype=torch.float64, device=torch_dev)
@@ -539,13 +531,9 @@ def test_ipm_iteration_cap_hands_over_to_riccati(path, torch_dev, monkeypatch):
         torch.cuda.synchronize()
         return out.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
 
-    monkeypatch.setenv("LMPC_DENSE", "ipm")
-    monkeypatch.setenv("LMPC_DENSE_ITER_CAP", "3")
-    gc, sc, ic = run()
-    monkeypatch.delenv("LMPC_DENSE_ITER_CAP")
-    gd, sd, idn = run()
-    monkeypatch.setenv("LMPC_DENSE", "0")
-    gr, sr, ir = run()
+    gc, sc, ic = run("ipm", 3)
+    gd, sd, idn = run("ipm")
+    gr, sr, ir = run("off")
     ref, _, fails = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
     assert fails == 0 and np.all(sc == 0) and np.all(sd == 0) and np.all(sr == 0)
     assert np.all((idn & 0xFFFF) > 3)                       # uncapped: every QP needs more than 3 iterations
@@ -553,14 +541,13 @@ def test_ipm_iteration_cap_hands_over_to_riccati(path, torch_dev, monkeypatch):
     assert rel_err(gc, ref) <= TOL_REGRESS and rel_err(gd, ref) <= TOL_REGRESS
 
 
-def test_mixed_streams_and_host_path_share_one_context(torch_dev, monkeypatch):
+def test_mixed_streams_and_host_path_share_one_context(torch_dev):
     """One context, three calls in flight: an asynchronous device solve on stream A (Riccati kernel: per-QP
     factor scratch), a host-pointer solve (the context's own stream, same scratch slots) issued before A has
     finished, then a device solve on stream B.  The context orders them, so each result equals the
     same solve run alone.  The caller's current device is left as it was."""
     import torch
 
-    monkeypatch.setenv("LMPC_DENSE", "0")
     p, H, rec, con = synth.config_batch(3, count=4096, first_index=1)    # H = 20: ~7 ms of Riccati kernel
     _, _, rec2, con2 = synth.config_batch(3, count=512, first_index=90001)
     _, _, rec3, con3 = synth.config_batch(3, count=2048, first_index=50001)

@@ -6,9 +6,9 @@ for tag in "$@"; do
   for spec in ${AB_SPECS:-2:20 2gi:20 2off:20 3:5 4:3 5:5}; do
     set -- ${spec/:/ }
     cfg=${1%gi}; cfg=${cfg%off}; steps=$2
-    env=""
-    case "$1" in *gi) env="LMPC_DENSE=gi";; *off) env="LMPC_DENSE=0";; esac
-    out=$(env $env LMPC_LIB=tools/build/liblmpc_$tag.so timeout -k 10 120 python bench.py --config $cfg --steps $steps --warmup 2 --no-cpu 2>/dev/null) || { echo "$tag config $1 FAILED"; exit 1; }
+    dense=""
+    case "$1" in *gi) dense="--dense gi";; *off) dense="--dense off";; esac
+    out=$(LMPC_LIB=tools/build/liblmpc_$tag.so timeout -k 10 120 python bench.py $dense --config $cfg --steps $steps --warmup 2 --no-cpu 2>/dev/null) || { echo "$tag config $1 FAILED"; exit 1; }
     echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', 'config', '$1', 'kernel_ms %.4f'%d['roofline']['kernel_ms'], 'QP/s %.3e'%d['value'], 'err %.1e'%d['max_grf_err'], d['qp_status'])"
   done
 done

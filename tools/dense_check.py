@@ -1,6 +1,5 @@
 #!/usr/bin/env python3
-"""Dev tool (GPU): the condensed dense path vs the Riccati path vs the oracle, and their kernel times.
-LMPC_DENSE is read at lmpc_create, so each solver below picks its path from the environment."""
+"""Dev tool (GPU): the condensed dense path vs the Riccati path vs the oracle, and their kernel times."""
 import os
 import sys
 import time
@@ -15,12 +14,11 @@ from legged_mpc_control_amd import BatchedConvexQPSolver, synth  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
-MODES = {"gi": "gi", "ipm": "ipm", "riccati": "0"}
+MODES = {"gi": "gi", "ipm": "ipm", "riccati": "off"}
 
 
 def solver(p, H, B, mode):
-    os.environ["LMPC_DENSE"] = MODES[mode]
-    return BatchedConvexQPSolver(p, H, B)
+    return BatchedConvexQPSolver(p, H, B, dense_path=MODES[mode])
 
 
 def main():

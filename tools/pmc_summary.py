@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Turn the output of tools/profile_round.sh (gpurun_out/prof) into the committed evidence:
-profiles/<tag>/{c2,c4}_kernel_stats.csv, pmc_per_dispatch.json, pmc_calibration.json, and
-profiles/pmc_traffic.json (bytes per launch for bench.py's roofline.traffic).
+profiles/<tag>/c{2,2gi,3,4,5}_kernel_stats.csv, pmc_per_dispatch.json, pmc_calibration.json,
+profiles/pmc_traffic.json (bytes per launch for bench.py's roofline.traffic) and profiles/pmc_flops.json
+(the fp64 flops the solve kernels execute per QP, for bench.py's roofline.executed):
+SQ_INSTS_VALU_FLOPS_FP64 (VALU flops) + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64 (matrix-core flops).
 
 Calibration (tools/ubench/pmc_cal.hip, 512 MiB past the Infinity Cache): for 8-byte-per-lane
 coalesced accesses, the access width the solve kernels use, FETCH_SIZE reports half the bytes read
@@ -26,8 +28,8 @@ def rows(name):
 SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_gi_kernel", "lmpc_qp_kernel")  # one solve launch = a dense-path kernel + the Riccati kernel
 
 
-def per_kernel(name, kern):
-    r = [x for x in rows(name) if kern in x["Kernel_Name"]]
+def per_kernel(name, kern, counter=None):
+    r = [x for x in rows(name) if kern in x["Kernel_Name"] and (counter is None or x["Counter_Name"] == counter)]
     return [float(x["Counter_Value"]) for x in r], [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in r]
 
 
@@ -74,7 +76,27 @@ def main():
 
     per = {}
     traffic = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-    for c, wl, qps in (("2", "go1_trot_h10_b1024", 1024), ("4", "go1_mixed_h10_b65536+terrain", 65536)):
+    fpath = os.path.join(ROOT, "profiles", "pmc_flops.json")
+    flops = json.load(open(fpath)) if os.path.exists(fpath) else {}
+    for c, wl, qps in (("2", "go1_trot_h10_b1024", 1024), ("4", "go1_mixed_h10_b65536+terrain", 65536),
+                       ("3", "go1_trot_h20_b8192", 8192), ("5", "go1_trot_h30_b4096", 4096)):
+        if not os.path.isdir(os.path.join(SRC, f"f{c}")):
+            continue
+        valu = mfma = 0.0
+        for kern in SOLVE_KERNELS:
+            v, _ = per_kernel(f"q{c}", kern, "SQ_INSTS_VALU_FLOPS_FP64")
+            m, _ = per_kernel(f"q{c}", kern, "SQ_INSTS_VALU_MFMA_MOPS_F64")
+            if v:
+                valu += st.mean(v)
+                mfma += 512 * st.mean(m)
+        flops[wl] = {
+            "flop_per_qp": (valu + mfma) / qps, "valu_flop_per_qp": valu / qps, "mfma_flop_per_qp": mfma / qps,
+            "source": f"profiles/{TAG}/q{c}_counter_collection.csv",
+            "method": f"rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_MFMA_MOPS_F64 over bench.py (config {c}, "
+                      "--no-cpu); per-dispatch means summed over the launch's solve kernels; MFMA flops = 512 x MOPS",
+        }
+        shutil.copy(os.path.join(SRC, f"q{c}", f"q{c}_counter_collection.csv"),
+                    os.path.join(DST, f"q{c}_counter_collection.csv"))
         fb = wb = 0.0
         per[wl] = {}
         for kern in SOLVE_KERNELS:
@@ -98,11 +120,17 @@ def main():
         }
     json.dump(per, open(os.path.join(DST, "pmc_per_dispatch.json"), "w"), indent=1)
     json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    json.dump(flops, open(fpath, "w"), indent=1)
     for c in ("c2", "c4", "c2gi", "c3", "c5"):
+        if not os.path.isdir(os.path.join(SRC, c)):
+            continue
         shutil.copy(os.path.join(SRC, c, f"{c}_kernel_stats.csv"), os.path.join(DST, f"{c}_kernel_stats.csv"))
         shutil.copy(os.path.join(SRC, f"{c}_bench.log"), os.path.join(DST, f"{c}_bench.log"))
     for k, v in traffic.items():
-        print(k, round(v["bytes_per_launch"] / 1e6, 1), "MB/launch")
+        print(k, round(v["bytes_per_launch"] / 1e6, 1), "MB/launch", round(v["bytes_per_qp"]), "B/QP")
+    for k, v in flops.items():
+        print(k, round(v["flop_per_qp"] / 1e6, 3), "Mflop/QP executed,", round(v["mfma_flop_per_qp"] / v["flop_per_qp"], 3),
+              "on the matrix cores")
 
 
 if __name__ == "__main__":
