@@ -4,6 +4,9 @@ profiles/<tag>/c{2,2gi,3,4,5}_kernel_stats.csv, pmc_per_dispatch.json, pmc_calib
 profiles/pmc_traffic.json (bytes per launch for bench.py's roofline.traffic) and profiles/pmc_flops.json
 (the fp64 flops the solve kernels execute per QP, for bench.py's roofline.executed):
 SQ_INSTS_VALU_FLOPS_FP64 (VALU flops) + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64 (matrix-core flops).
+The flop counters are calibrated the same way (pmc_cal's fma64 / mfma64 kernels, known counts): on gfx950
+SQ_INSTS_VALU_FLOPS_FP64 counts an instruction's flops once per wave, whatever its exec mask (x64 = the
+lane-flops the wave issues, an upper bound on the useful ones), and a 16x16x4 f64 MFMA is 4 MOPS (x512 = 2048).
 
 Calibration (tools/ubench/pmc_cal.hip, 512 MiB past the Infinity Cache): for 8-byte-per-lane
 coalesced accesses, the access width the solve kernels use, FETCH_SIZE reports half the bytes read
@@ -72,6 +75,14 @@ def main():
     write_factor = truth_kib / cal["write8:WRITE_SIZE_KiB"]
     cal.update(read_factor=read_factor, write_factor=write_factor, bytes_moved=truth_kib * 1024,
                note="8 B/lane coalesced; FETCH_SIZE x read_factor and WRITE_SIZE x write_factor = bytes")
+    # fp64 flop counters: fma64 (1024 waves x 4 chains x 4096 FMAs, all lanes) and mfma64 (1024 x 1024 MFMAs)
+    qf = {x["Counter_Name"]: float(x["Counter_Value"]) for x in rows("calq") if x["Kernel_Name"].startswith("fma64")}
+    qm = {x["Counter_Name"]: float(x["Counter_Value"]) for x in rows("calq") if x["Kernel_Name"].startswith("mfma64")}
+    valu_factor = (2.0 * 4 * 4096 * 64 * 1024) / qf["SQ_INSTS_VALU_FLOPS_FP64"]
+    mfma_factor = (2048.0 * 1024 * 1024) / qm["SQ_INSTS_VALU_MFMA_MOPS_F64"]
+    cal.update(valu_flop_factor=valu_factor, mfma_flop_factor=mfma_factor,
+               flop_note="SQ_INSTS_VALU_FLOPS_FP64 x valu_flop_factor = lane-flops issued (exec mask ignored by the "
+                         "counter); SQ_INSTS_VALU_MFMA_MOPS_F64 x mfma_flop_factor = matrix-core flops")
     json.dump(cal, open(os.path.join(DST, "pmc_calibration.json"), "w"), indent=1)
 
     per = {}
@@ -87,13 +98,15 @@ def main():
             v, _ = per_kernel(f"q{c}", kern, "SQ_INSTS_VALU_FLOPS_FP64")
             m, _ = per_kernel(f"q{c}", kern, "SQ_INSTS_VALU_MFMA_MOPS_F64")
             if v:
-                valu += st.mean(v)
-                mfma += 512 * st.mean(m)
+                valu += valu_factor * st.mean(v)
+                mfma += mfma_factor * st.mean(m)
         flops[wl] = {
             "flop_per_qp": (valu + mfma) / qps, "valu_flop_per_qp": valu / qps, "mfma_flop_per_qp": mfma / qps,
             "source": f"profiles/{TAG}/q{c}_counter_collection.csv",
             "method": f"rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_MFMA_MOPS_F64 over bench.py (config {c}, "
-                      "--no-cpu); per-dispatch means summed over the launch's solve kernels; MFMA flops = 512 x MOPS",
+                      f"--no-cpu); per-dispatch means summed over the launch's solve kernels; VALU = {valu_factor:.1f} x "
+                      f"FLOPS_FP64 (lane-flops issued: the counter ignores the exec mask), MFMA = {mfma_factor:.1f} x MOPS; "
+                      f"factors from profiles/{TAG}/pmc_calibration.json",
         }
         shutil.copy(os.path.join(SRC, f"q{c}", f"q{c}_counter_collection.csv"),
                     os.path.join(DST, f"q{c}_counter_collection.csv"))

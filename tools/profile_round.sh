@@ -27,7 +27,8 @@ for c in $CFGS; do
 done
 if [ $rc = 0 ]; then
   pmc --pmc FETCH_SIZE --kernel-trace -d $OUT/calf -o calf --output-format csv -- tools/ubench/pmc_cal > $OUT/calf.log 2>&1 &&
-  pmc --pmc WRITE_SIZE --kernel-trace -d $OUT/calw -o calw --output-format csv -- tools/ubench/pmc_cal > $OUT/calw.log 2>&1
+  pmc --pmc WRITE_SIZE --kernel-trace -d $OUT/calw -o calw --output-format csv -- tools/ubench/pmc_cal > $OUT/calw.log 2>&1 &&
+  pmc --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_MFMA_MOPS_F64 --kernel-trace -d $OUT/calq -o calq --output-format csv -- tools/ubench/pmc_cal > $OUT/calq.log 2>&1
   rc=$?
 fi
 echo "profile_round rc=$rc"
