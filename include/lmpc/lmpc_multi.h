@@ -8,8 +8,8 @@
  * of a node without PyTorch: bench.py's torch.distributed path (one process per GPU) and this one
  * (one process, one communicator per device from ncclCommInitAll) shard identically.
  *
- * Sharding: device r of R owns the contiguous QPs [first_r, first_r + count_r) of the batch
- * (lmpc_multi_shard: sizes differ by at most one, the first batch % R shards one larger).  Every QP is
+ * Sharding: device r of R owns the contiguous QPs [batch r / R, batch (r+1) / R) of the batch
+ * (lmpc_multi_shard; sizes differ by at most one; the same split as bench.py's fixed-batch config 4).  Every QP is
  * independent, so a QP's answer is bit-identical whatever the device count (the single-device path's
  * kernels run on each shard; the choice of kernel instance never changes a result bit).
  *

@@ -44,6 +44,15 @@ HOQP_SYMBOLS = (
     "lmpc_hoqp_solve_device", "lmpc_hoqp_sync", "lmpc_wbc_tasks", "lmpc_wbc_tasks_device",
 )
 HOQP_MAX_LEVELS = 4
+# include/lmpc/lmpc_multi.h: one process, several GPUs (liblmpc_multi.so, RCCL scatter / gather)
+MULTI_LIB_PATH = os.path.join(_HERE, "lib", "liblmpc_multi.so")
+MULTI_SYMBOLS = (
+    "lmpc_multi_abi_version", "lmpc_multi_shard", "lmpc_multi_create", "lmpc_multi_destroy", "lmpc_multi_num_devices",
+    "lmpc_multi_set_options", "lmpc_multi_set_dense_path", "lmpc_multi_solve_commands_device",
+    "lmpc_multi_solve_synth_device", "lmpc_multi_solve_commands",
+)
+MULTI_ABI_VERSION = 1
+LMPC_ERR_COMM = -6
 
 
 class LmpcParams(ctypes.Structure):
@@ -272,6 +281,48 @@ def lib():
         return L
 
 
+_mlib = None
+
+
+def multi_lib():
+    """Load liblmpc_multi.so (raises NativeLibraryError if it was not built)."""
+    global _mlib
+    lib()  # liblmpc.so first: the multi-device library links it
+    with _lock:
+        if _mlib is not None:
+            return _mlib
+        if not os.path.exists(MULTI_LIB_PATH):
+            raise NativeLibraryError(f"{MULTI_LIB_PATH} not found: build it with __graft_entry__.build()")
+        M = ctypes.CDLL(MULTI_LIB_PATH)
+        vp, i32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)
+        pp = ctypes.POINTER(LmpcParams)
+        M.lmpc_multi_abi_version.restype = ctypes.c_int
+        M.lmpc_multi_shard.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p, i32p]
+        M.lmpc_multi_shard.restype = None
+        M.lmpc_multi_create.argtypes = [pp, ctypes.c_int, i32p, ctypes.c_int, ctypes.POINTER(vp)]
+        M.lmpc_multi_create.restype = ctypes.c_int
+        M.lmpc_multi_destroy.argtypes = [vp]
+        M.lmpc_multi_destroy.restype = None
+        M.lmpc_multi_num_devices.argtypes = [vp]
+        M.lmpc_multi_num_devices.restype = ctypes.c_int
+        M.lmpc_multi_set_options.argtypes = [vp, ctypes.POINTER(LmpcOptions)]
+        M.lmpc_multi_set_options.restype = ctypes.c_int
+        M.lmpc_multi_set_dense_path.argtypes = [vp, ctypes.c_int]
+        M.lmpc_multi_set_dense_path.restype = ctypes.c_int
+        M.lmpc_multi_solve_commands_device.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
+        M.lmpc_multi_solve_commands_device.restype = ctypes.c_int
+        M.lmpc_multi_solve_synth_device.argtypes = [vp, ctypes.POINTER(LmpcSynthCfg), ctypes.c_uint64, ctypes.c_int64,
+                                                    ctypes.c_int, ctypes.c_double, vp, vp, vp]
+        M.lmpc_multi_solve_synth_device.restype = ctypes.c_int
+        M.lmpc_multi_solve_commands.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp, vp]
+        M.lmpc_multi_solve_commands.restype = ctypes.c_int
+        if M.lmpc_multi_abi_version() != MULTI_ABI_VERSION:
+            raise NativeLibraryError("liblmpc_multi.so ABI version mismatch")
+        _mlib = M
+        return M
+
+
 def check(rc: int, what: str = "lmpc") -> None:
     if rc != LMPC_OK:
-        raise RuntimeError(f"{what} failed: {lib().lmpc_strerror(rc).decode()} ({rc})")
+        msg = "RCCL communication failed" if rc == LMPC_ERR_COMM else lib().lmpc_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed: {msg} ({rc})")

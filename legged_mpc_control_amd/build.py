@@ -54,6 +54,27 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+MULTI_LIB = os.path.join(LIBDIR, "liblmpc_multi.so")
+
+
+def build_multi(force: bool = False, verbose: bool = False) -> str:
+    """liblmpc_multi.so (include/lmpc/lmpc_multi.h): several devices from one process, RCCL for the batch
+    scatter / gather.  Links liblmpc.so (found next to it at run time) and librccl."""
+    src = os.path.join(CSRC, "lmpc_multi.cpp")
+    deps = [src, LIB, os.path.join(ROOT, "include", "lmpc", "lmpc_multi.h"), os.path.join(ROOT, "include", "lmpc", "lmpc.h"),
+            os.path.abspath(__file__)]
+    if not force and not _stale(MULTI_LIB, deps):
+        return MULTI_LIB
+    tmp = MULTI_LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O2", "-fPIC", "-shared", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", tmp, src,
+           "-L", LIBDIR, "-llmpc", "-Wl,-rpath,$ORIGIN", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, MULTI_LIB)
+    return MULTI_LIB
+
+
 def build_stamps(force: bool = False) -> str:
     """Diagnostic library with in-kernel phase cycle stamps (tools/stamps_probe.py); never shipped as the product."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
@@ -93,6 +114,19 @@ def build_cpp_test(force: bool = False) -> str:
     return out
 
 
+def build_cpp_multi_test(force: bool = False) -> str:
+    """C++ host over the multi-device C-ABI (tests/cpp/multi_test.cpp): shards a batch without PyTorch."""
+    src = os.path.join(ROOT, "tests", "cpp", "multi_test.cpp")
+    out = os.path.join(ROOT, "tests", "cpp", "build", "multi_test")
+    if not force and not _stale(out, [src, LIB, MULTI_LIB]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", out, src,
+           "-L", LIBDIR, "-llmpc_multi", "-llmpc", f"-Wl,-rpath,{LIBDIR}"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_cpp_hoqp_test(force: bool = False) -> str:
     """C++ program running the reference's HoQp test (ho_qp_test.cpp) against legged::HoQp (include/lmpc/HoQp.hpp)."""
     src = os.path.join(ROOT, "tests", "cpp", "ho_qp_test.cpp")
@@ -122,3 +156,4 @@ def build_tool_cpp(name: str, force: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build_native(force=True, verbose=True))
+    print(build_multi(force=True, verbose=True))

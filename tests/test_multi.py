@@ -1,0 +1,162 @@
+"""The multi-device C-ABI (include/lmpc/lmpc_multi.h, liblmpc_multi.so): a C++ host shards a batch over the
+GPUs of a node, RCCL only for the scatter / gather.
+
+CPU: the library loads and exports every declared symbol, the shard split is bench.py's, bad arguments are
+rejected without a GPU.  GPU (one device on the test box): every entry point is bit-identical to the
+single-device C-ABI (lmpc_solve_commands_device) on the same instances, and the C++ program
+tests/cpp/multi_test.cpp shards without PyTorch.  More than one device needs a multi-GPU node (the driver's
+scaling runs); the split and the per-shard solves are what those add, and both are covered here.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+from legged_mpc_control_amd import _native as N
+from legged_mpc_control_amd import dist as D
+
+HEADER = os.path.join(ROOT, "include", "lmpc", "lmpc_multi.h")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _multi_built():
+    from legged_mpc_control_amd import build as B
+
+    B.build_multi()
+
+
+def declared():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(lmpc_multi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declarations_are_exported():
+    M = N.multi_lib()
+    for name in declared():
+        assert hasattr(M, name), name
+    assert sorted(N.MULTI_SYMBOLS) == declared()
+    out = subprocess.run(["nm", "-D", "--defined-only", N.MULTI_LIB_PATH], capture_output=True, text=True, check=True)
+    syms = {l.split()[-1] for l in out.stdout.splitlines() if l.strip()}
+    assert set(declared()) <= syms  # C linkage
+    assert M.lmpc_multi_abi_version() == 1
+
+
+@pytest.mark.parametrize("batch", [0, 1, 7, 1024, 65536, 65537])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_shard_split_is_benchs(batch, n):
+    from legged_mpc_control_amd.multi import shard
+
+    end = 0
+    for r in range(n):
+        f, c = shard(batch, n, r)
+        lo, hi = D.split_range(r, n, batch)
+        assert (f, c) == (lo, hi - lo)
+        assert f == end and c >= 0
+        end = f + c
+    assert end == batch
+
+
+def test_create_rejects_bad_arguments():
+    M = N.multi_lib()
+    p = N.LmpcParams()
+    N.lib().lmpc_params_go1(ctypes.byref(p))
+    m = ctypes.c_void_p()
+    dup = (ctypes.c_int32 * 2)(0, 0)
+    assert M.lmpc_multi_create(ctypes.byref(p), 10, dup, 2, ctypes.byref(m)) == -1   # same device twice
+    one = (ctypes.c_int32 * 1)(0)
+    assert M.lmpc_multi_create(ctypes.byref(p), 10, one, 0, ctypes.byref(m)) == -1   # no device
+    assert M.lmpc_multi_create(None, 10, one, 1, ctypes.byref(m)) == -1
+    assert M.lmpc_multi_solve_commands_device(None, None, None, 4, None, None, None, None) == -1
+    assert M.lmpc_multi_num_devices(None) == -1
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    M = N.multi_lib()
+    p = N.LmpcParams()
+    N.lib().lmpc_params_go1(ctypes.byref(p))
+    m = ctypes.c_void_p()
+    one = (ctypes.c_int32 * 1)(0)
+    assert M.lmpc_multi_create(ctypes.byref(p), 10, one, 1, ctypes.byref(m)) == -2  # LMPC_ERR_DEVICE
+    assert not m.value
+
+
+# ---------------------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("cid", [2, 4])
+def test_multi_paths_equal_single_device(cid):
+    """lmpc_multi over one device: device-pointer commands, synthetic shards and host commands all give the
+    single-device C-ABI's bits (configs 2 and 4, config 4 with terrain normals)."""
+    import torch
+
+    from legged_mpc_control_amd import BatchedConvexQPSolver, synth
+    from legged_mpc_control_amd.multi import MultiDeviceSolver
+
+    dev = torch.device("cuda:0")
+    cfgd = synth.CONFIGS[cid]
+    H = cfgd["H"]
+    B = 2048
+    p = synth.params(cfgd["robot"])
+    seed = synth.BASE_SEED + cid
+    terrain = cid == 4
+    single = BatchedConvexQPSolver(p, H, max_batch=0, device=0, dense_path="gi" if terrain else "ipm")
+    cmd = single.synth_commands_device(synth.config_cfg(cid), B, seed, first_index=100, device=dev)
+    nrm = single.synth_normals_device(B, seed, first_index=100, device=dev) if terrain else None
+    g1 = torch.empty((B, H, 12), dtype=torch.float64, device=dev)
+    s1 = torch.empty(B, dtype=torch.int32, device=dev)
+    i1 = torch.empty(B, dtype=torch.int32, device=dev)
+    single.solve_commands_device(cmd, g1, s1, i1, normals=nrm)
+    torch.cuda.synchronize()
+    assert torch.all(s1 == 0)
+
+    m = MultiDeviceSolver(p, H, [0], dense_path="gi" if terrain else "ipm")
+    assert m.num_devices == 1
+    g2 = torch.empty_like(g1)
+    s2 = torch.empty_like(s1)
+    i2 = torch.empty_like(i1)
+    m.solve_commands_device(cmd, g2, s2, i2, d_normals=nrm)
+    assert torch.equal(g1, g2) and torch.equal(s1, s2) and torch.equal(i1, i2)
+    g3, s3, i3 = m.solve_synth_device(synth.config_cfg(cid), B, seed, first_index=100,
+                                      theta_max=synth.TERRAIN_THETA_MAX if terrain else -1.0)
+    assert torch.equal(g1, g3) and torch.equal(s1, s3) and torch.equal(i1, i3)
+    g4, s4, i4 = m.solve_commands(cmd.cpu().numpy(), None if nrm is None else nrm.cpu().numpy())
+    assert np.array_equal(g4, g1.cpu().numpy()) and np.array_equal(s4, s1.cpu().numpy())
+    m.close()
+
+
+@pytest.mark.gpu
+def test_cpp_host_shards_without_torch():
+    """tests/cpp/multi_test.cpp: a C++ host over lmpc_multi.h on every visible device; its GRF checksum equals the
+    single-device solve of the same synthetic batch (generated from (seed, global index) on each device)."""
+    import torch
+
+    from legged_mpc_control_amd import BatchedConvexQPSolver, synth
+    from legged_mpc_control_amd import build as B
+
+    exe = B.build_cpp_multi_test()
+    ndev = torch.cuda.device_count()
+    batch, seed = 3000, 20261017
+    out = subprocess.run([exe, str(ndev), str(batch), str(seed)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    # the last line is the program's (RCCL may print its own banner first)
+    n, b, ms, bad, it0, csum = out.stdout.strip().splitlines()[-1].split()
+    assert int(n) == ndev and int(b) == batch and int(bad) == 0
+    p = synth.params("go1")
+    s = BatchedConvexQPSolver(p, 10, max_batch=0, device=0)
+    dev = torch.device("cuda:0")
+    cmd = s.synth_commands_device(synth.synth_cfg("go1", 0), batch, seed, first_index=0, device=dev)
+    g = torch.empty((batch, 10, 12), dtype=torch.float64, device=dev)
+    it = torch.empty(batch, dtype=torch.int32, device=dev)
+    s.solve_commands_device(cmd, g, iters=it)
+    torch.cuda.synchronize()
+    ref = g.cpu().numpy()
+    assert int(it0) == int(it[0].item())
+    assert float(csum) == pytest.approx(float(ref.sum()), rel=1e-12, abs=1e-9)
