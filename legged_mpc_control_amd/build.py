@@ -127,6 +127,22 @@ def build_cpp_multi_test(force: bool = False) -> str:
     return out
 
 
+def build_cpp_eigen_test(force: bool = False) -> str:
+    """The reference's ConvexMpc lines over include/lmpc/ConvexQPSolverEigen.hpp (tests/cpp/eigen_dropin_test.cpp),
+    compiled against the test stand-ins in tests/cpp/eigen_dropin/ (no Eigen / ROS in this image)."""
+    src = os.path.join(ROOT, "tests", "cpp", "eigen_dropin_test.cpp")
+    stub = os.path.join(ROOT, "tests", "cpp", "eigen_dropin")
+    out = os.path.join(ROOT, "tests", "cpp", "build", "eigen_dropin_test")
+    hdr = os.path.join(ROOT, "include", "lmpc", "ConvexQPSolverEigen.hpp")
+    if not force and not _stale(out, [src, hdr, LIB]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), "-O2", "-std=c++17", "-Wall", "-I", stub, "-I", os.path.join(ROOT, "include"), "-o", out, src,
+           "-L", LIBDIR, "-llmpc", f"-Wl,-rpath,{LIBDIR}"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_cpp_hoqp_test(force: bool = False) -> str:
     """C++ program running the reference's HoQp test (ho_qp_test.cpp) against legged::HoQp (include/lmpc/HoQp.hpp)."""
     src = os.path.join(ROOT, "tests", "cpp", "ho_qp_test.cpp")

@@ -130,6 +130,24 @@ int oracle_predict_contact(int gait, int leg, double gait_phase, double gait_spe
  * advanced to that phase: first pattern entry whose switch time is > phase). */
 int oracle_current_contact(int gait, int leg, double gait_phase);
 
+/* The reference's own algorithm, OSQP's ADMM (osqp_admm.c; restated from its published algorithm, see there),
+ * with the reference's settings by default (ConvexQPSolver.cpp:182-194).  Dense row-major A in, CSR inside. */
+typedef struct oracle_osqp_settings {
+    double eps_abs, eps_rel, rho, sigma, alpha;
+    int scaling, max_iter, check_termination, adaptive_rho_interval;
+} oracle_osqp_settings;
+void oracle_osqp_settings_default(oracle_osqp_settings* s);
+/* min 1/2 x'diag(P)x + q'x  s.t. l <= A x <= u; info[3] (optional) = final primal / dual residual, rho.
+ * Returns 0 ok, -1 allocation, -2 factorisation failed. */
+int oracle_osqp_solve(int n, int m, const double* P_diag, const double* q, const double* A, const double* l,
+                      const double* u, const oracle_osqp_settings* s, double* x, int* iters, int* converged,
+                      double info[3]);
+/* compute_grfs over a batch: the reference's sparse QP (oracle_build_sparse_qp_ex) -> ADMM -> u_0..u_{H-1}
+ * (grf[b][H][12]; NaN -> zeros); iters / converged may be NULL; s NULL = the reference's settings. */
+int oracle_osqp_grf_batch(const oracle_params* p, int H, int batch, const double* rec, const uint8_t* contact,
+                          const double* normals, const oracle_osqp_settings* s, double* grf, int32_t* iters,
+                          int32_t* converged, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,10 +34,17 @@ class OracleParams(ctypes.Structure):
     ]
 
 
+class OsqpSettings(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("eps_abs", "eps_rel", "rho", "sigma", "alpha")] + \
+               [(k, ctypes.c_int) for k in ("scaling", "max_iter", "check_termination", "adaptive_rho_interval")]
+
+
 def build(force: bool = False) -> str:
     """Compile the oracle with gcc (make) into oracle/build/ (make rebuilds it when the sources changed)."""
-    src = os.path.join(_HERE, "lmpc_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or (os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_LIB_PATH)):
+    srcs = [os.path.join(_HERE, f) for f in ("lmpc_oracle.c", "osqp_admm.c", "lmpc_oracle.h")]
+    stale = not os.path.exists(_LIB_PATH) or any(
+        os.path.exists(s) and os.path.getmtime(s) > os.path.getmtime(_LIB_PATH) for s in srcs)
+    if force or stale:
         subprocess.run(["make", "-s", "-C", _HERE] + (["-B"] if force else []), check=True)
     return _LIB_PATH
 
@@ -83,6 +90,14 @@ def lib():
             L.oracle_predict_contact.restype = ctypes.c_int
             L.oracle_current_contact.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
             L.oracle_current_contact.restype = ctypes.c_int
+            sp = ctypes.POINTER(OsqpSettings)
+            L.oracle_osqp_settings_default.argtypes = [sp]
+            L.oracle_osqp_settings_default.restype = None
+            L.oracle_osqp_solve.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, sp, dp, ip, ip, dp]
+            L.oracle_osqp_solve.restype = ctypes.c_int
+            L.oracle_osqp_grf_batch.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, u8p, dp, sp, dp, i32p, i32p,
+                                                ctypes.c_int]
+            L.oracle_osqp_grf_batch.restype = ctypes.c_int
             _lib = L
     return _lib
 
@@ -222,3 +237,37 @@ def grf_to_torque(rho_fix, rho_opt, rot, joint_pos, grf0) -> np.ndarray:
     lib().oracle_grf_to_torque(_dp(rf), _dp(ro), _dp(_f64(rot, 9)), _dp(_f64(joint_pos, 12)), _dp(_f64(grf0, 12)),
                                _dp(tau))
     return tau
+
+
+def osqp_settings(**kw) -> OsqpSettings:
+    """The reference's OSQP settings (ConvexQPSolver.cpp:182-194 + OSQP 0.6 defaults), fields overridable."""
+    s = OsqpSettings()
+    lib().oracle_osqp_settings_default(ctypes.byref(s))
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def osqp_solve(P_diag, q, A, l, u, **kw):
+    """C restatement of OSQP's ADMM (osqp_admm.c) on one QP -> (x, iters, converged, [prim, dual, rho])."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    m, n = A.shape
+    x = np.zeros(n); info = np.zeros(3); it = ctypes.c_int(0); cv = ctypes.c_int(0)
+    rc = lib().oracle_osqp_solve(n, m, _dp(_f64(P_diag)), _dp(_f64(q)), _dp(A), _dp(_f64(l)), _dp(_f64(u)),
+                                 ctypes.byref(osqp_settings(**kw)), _dp(x), ctypes.byref(it), ctypes.byref(cv), _dp(info))
+    if rc != 0:
+        raise RuntimeError(f"oracle_osqp_solve failed: {rc}")
+    return x, it.value, bool(cv.value), info
+
+
+def osqp_grf_batch(p: OracleParams, H: int, rec, contact, n_threads: int = 1, normals=None, **kw):
+    """The reference's compute_grfs (OSQP ADMM at its settings) over a batch -> (grf [B,H,12], iters, converged)."""
+    B = rec.shape[0]
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    nrm, nrm_p = _normals(normals, (B,))
+    grf = np.zeros((B, H, 12)); it = np.zeros(B, dtype=np.int32); cv = np.zeros(B, dtype=np.int32)
+    i32 = ctypes.POINTER(ctypes.c_int32)
+    lib().oracle_osqp_grf_batch(ctypes.byref(p), H, B, _dp(rec), _u8p(contact), nrm_p, ctypes.byref(osqp_settings(**kw)),
+                                _dp(grf), it.ctypes.data_as(i32), cv.ctypes.data_as(i32), n_threads)
+    return grf, it, cv.astype(bool)

@@ -87,6 +87,20 @@ def test_cpp_dropin_program_builds():
     assert os.path.exists(exe) and os.access(exe, os.X_OK)
 
 
+def test_eigen_signature_header_compiles_with_reference_call_sites():
+    """include/lmpc/ConvexQPSolverEigen.hpp compiles under the reference's ConvexMpc constructor and grf_update lines
+    (tests/cpp/eigen_dropin_test.cpp, against test stand-ins of Eigen and the reference headers)."""
+    from legged_mpc_control_amd import build as B
+
+    exe = B.build_cpp_eigen_test(force=True)
+    assert os.path.exists(exe) and os.access(exe, os.X_OK)
+    src = open(os.path.join(ROOT, "tests", "cpp", "eigen_dropin_test.cpp")).read()
+    # the reference's own lines (ConvexMpc.cpp:13-14,70-72), verbatim
+    assert "fastConvex = ConvexQPSolver(state.param.q_weights," in src
+    assert "fastConvex.calc_mpc_reference(state, leg_FSM);" in src
+    assert "Eigen::Matrix<double, DIM_GRF, 1> qp_solution = fastConvex.compute_grfs(state);" in src
+
+
 def test_no_oracle_in_product_path():
     """The product package must never import or link the oracle (the checker)."""
     pkg = os.path.join(ROOT, "legged_mpc_control_amd")

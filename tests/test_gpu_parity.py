@@ -614,3 +614,31 @@ def test_python_dropin_warm_ticks_match_oracle():
         for i in range(4):
             fsm[i].gait_phase = (fsm[i].gait_phase + 4.0 * 0.01) % 1.0
     assert ipm[0] > 0 and min(ipm[1:]) == 0  # tick 0 cold; later ticks start from the shifted verified set
+
+
+def test_eigen_signature_dropin_vs_oracle():
+    """include/lmpc/ConvexQPSolverEigen.hpp under the reference's own ConvexMpc lines (ConvexMpc.cpp:13-14,70-75,
+    tests/cpp/eigen_dropin_test.cpp; Eigen and the reference headers are test stand-ins here): u_0 of every tick equals
+    the oracle's on the record and schedule the program reports, the horizon is the reference's PLAN_HORIZON (30),
+    v_d_world is written back (ConvexQPSolver.cpp:260), and warm-started later ticks need fewer iterations."""
+    from legged_mpc_control_amd import build as B
+
+    exe = B.build_cpp_eigen_test()
+    out = subprocess.run([exe, "3"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.strip().splitlines()
+    p = synth.params("go1")
+    op = O.params_from(p)
+    H = 30
+    assert len(lines) == 15
+    for i in range(0, len(lines), 5):
+        assert lines[i].endswith("status 0")
+        rec = np.array(lines[i + 1].split()[1:], dtype=np.float64)
+        con = np.array(lines[i + 2].split()[1:], dtype=np.uint8).reshape(H, 4)
+        vdw = np.array(lines[i + 3].split()[1:], dtype=np.float64)
+        u0 = np.array(lines[i + 4].split()[1:], dtype=np.float64)
+        assert rec.size == 33 + 12 * H
+        R = rec[12:21].reshape(3, 3)
+        np.testing.assert_allclose(vdw, R @ np.array([0.4, 0.0, 0.0]), rtol=0, atol=1e-15)
+        ref, _, _ = O.solve(op, H, rec, con)
+        assert rel_err(u0, ref[0]) <= TOL_REGRESS

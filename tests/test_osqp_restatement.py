@@ -57,3 +57,28 @@ def test_reference_settings_give_an_approximate_optimum():
     assert min(gaps) > -1e-9          # the exact optimum is never beaten
     assert max(gaps) < 0.1            # OSQP is close in objective ...
     assert max(du0) > 1.0             # ... but not in force space
+
+
+@pytest.mark.parametrize("name", ["config2", "config4t", "config5"])
+def test_c_admm_restatement_matches_numpy(name):
+    """oracle/osqp_admm.c (the CPU baseline bench.py times as the reference's algorithm) takes the numpy
+    restatement's iterates: same termination iteration, same point to rounding (it solves the reduced KKT system
+    by an envelope Cholesky instead of numpy's dense one), on flat and terrain instances."""
+    p, g = _golden(name)
+    op = O.params_from(p)
+    H = g["H"]
+    for b in range(min(3, g["rec"].shape[0])):
+        nrm = None if g["normals"] is None else g["normals"][b]
+        P, q, A, l, u = O.build_sparse_qp(op, H, g["rec"][b], g["contact"][b], nrm)
+        xr, info = Q.solve(P, q, A, l, u)
+        xc, it, cv, _ = O.osqp_solve(P, q, A, l, u)
+        assert it == info["iters"] and cv == info["converged"]
+        assert np.max(np.abs(xc - xr)) <= 1e-6 * max(1.0, np.max(np.abs(xr)))
+    # the batch entry point returns each instance's u_0..u_{H-1}, as Q.grf does
+    B = min(4, g["rec"].shape[0])
+    grf, iters, conv = O.osqp_grf_batch(op, H, g["rec"][:B], g["contact"][:B], n_threads=2,
+                                        normals=None if g["normals"] is None else g["normals"][:B])
+    for b in range(B):
+        gr, info = Q.grf(op, H, g["rec"][b], g["contact"][b], None if g["normals"] is None else g["normals"][b])
+        assert iters[b] == info["iters"] and conv[b]
+        assert np.max(np.abs(grf[b] - gr)) <= 1e-6 * max(1.0, np.max(np.abs(gr)))
