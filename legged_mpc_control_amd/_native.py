@@ -138,7 +138,8 @@ class LmpcHoqpDims(ctypes.Structure):
 
 
 class LmpcHoqpOptions(ctypes.Structure):
-    _fields_ = [("max_iter", ctypes.c_int32), ("tol_mu", ctypes.c_double), ("tol_res", ctypes.c_double)]
+    _fields_ = [("max_iter", ctypes.c_int32), ("tol_mu", ctypes.c_double), ("tol_res", ctypes.c_double),
+                ("crossover", ctypes.c_int32)]
 
 
 class LmpcWbcInput(ctypes.Structure):

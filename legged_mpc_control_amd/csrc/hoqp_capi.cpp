@@ -90,12 +90,13 @@ void fill_dev(lmpc::HoqpDev& P, const lmpc_hoqp_dims* d) {
     P.rec_len = off;
     P.slack_len = stacked;
     P.kmax = mmax > P.np ? mmax : P.np;
-    P.scratch_len = 2 * (int64_t)P.n * P.np + (int64_t)P.np * P.np;
+    P.scratch_len = 2 * (int64_t)P.n * P.np + 2 * (int64_t)P.np * P.np;  // Z, Z', Hy, crossover T
     lmpc_hoqp_options o;
     lmpc_hoqp_options_default(&o);
     P.max_iter = o.max_iter;
     P.tol_mu = o.tol_mu;
     P.tol_res = o.tol_res;
+    P.crossover = o.crossover;
 }
 
 hipError_t ensure_scratch(lmpc_hoqp_ctx* c, int batch) {
@@ -152,6 +153,7 @@ void lmpc_hoqp_options_default(lmpc_hoqp_options* o) {
     o->max_iter = 60;
     o->tol_mu = 1e-13;
     o->tol_res = 1e-7;
+    o->crossover = 1;
 }
 
 int64_t lmpc_hoqp_lds_bytes(const lmpc_hoqp_dims* d) {
@@ -220,10 +222,13 @@ void lmpc_hoqp_destroy(lmpc_hoqp_ctx* c) {
 }
 
 int lmpc_hoqp_set_options(lmpc_hoqp_ctx* c, const lmpc_hoqp_options* o) {
-    if (!c || !o || o->max_iter < 1 || !(o->tol_mu > 0.0) || !(o->tol_res > 0.0)) return LMPC_ERR_ARG;
+    if (!c || !o || o->max_iter < 1 || !(o->tol_mu > 0.0) || !(o->tol_res > 0.0) || o->crossover < 0 ||
+        o->crossover > 1)
+        return LMPC_ERR_ARG;
     c->P.max_iter = o->max_iter;
     c->P.tol_mu = o->tol_mu;
     c->P.tol_res = o->tol_res;
+    c->P.crossover = o->crossover;
     return LMPC_OK;
 }
 

@@ -712,6 +712,211 @@ __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS
     gemm_xz<NP>(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
 }
 
+// Exact crossover (round 3) after an interior point that stopped short of its clean criterion (degenerate
+// rows whose slack and multiplier both vanish, a non-finite direction, the iteration cap): the level's KKT
+// system on the active set the iterate identifies (prototyped step for step in tools/hoqp_proto.py, EXACT=1):
+//   frozen rows (r < p) active where z > s:        R_A y = h_A, multipliers lambda_A >= 0
+//   own rows (r >= p) violated where zg > sg (the row constraint D y - v <= g, not v >= 0: for an inactive own
+//   row both v and its multiplier vanish):           the penalty 1/2 (R_r y - g_r)^2, i.e. R_r'R_r in the matrix
+// solved as a correction from the iterate y_i, so that where K is singular to rounding (Hy is along ker G: the
+// level's objective is flat there) the floored pivots keep the iterate's components, which satisfy the inactive
+// rows:  K_A = Hy + sum_violated R_r'R_r + rho R_A'R_A (an augmented-Lagrangian term: the same constrained
+// optimum, and K_A invertible where only the active rows bind), d0 = K_A^-1 (rhs - K_A y_i), y0 = y_i + d0,
+// T = K_A^-1 R_A' (one solve per active row), (R_A T) lambda = R_A y0 - h_A (LDL' with the same pivot floor),
+// y = y0 - T lambda.  The classification is repaired for up to XO_ROUNDS rounds -- the most negative multiplier
+// out, the most violated inactive frozen row in, own rows moved to the side they land on -- and the answer is
+// taken only if it then verifies: lambda >= 0, every row on its side, and the stationarity residual
+// Hy y + c + R'z within 1e-9 of the level's scale; otherwise the iterate is kept.  Returns the verdict
+// (uniform); on success S.y holds the exact y.  The reference solves each level exactly with qpOASES
+// (HoQp.cpp:158-174), an active-set method: this makes the degenerate levels exact too.
+constexpr int XO_ROUNDS = 6;
+template <int NP>
+__device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS& S_, int p, int nr, int nd, double bd0,
+                                                    double bd1, int fl0, int fl1, double scale, const gdouble* Hg,
+                                                    gdouble* Tg, int lane) {
+    const HS S = S_;
+    const HoqpDev P = uniform(P_);
+    p = uni(p);
+    nr = uni(nr);
+    nd = uni(nd);
+    const int ls = hq_ls(P), np = P.np;
+    const double bd[2] = {bd0, bd1};
+    int fl[2] = {fl0, fl1};  // bit 0: frozen row active, bit 1: own row violated
+    const double yi = lane < nd ? (double)S.y[lane] : 0.0;  // the interior-point iterate (S.y kept until success)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int r = lane + 64 * k;
+        if (r < P.rmax) S.t[r] = r < nr ? bd[k] : 0.0;  // every row's bound, for the lanes that own its Schur row
+    }
+    const double rho = fmax(1.0, wave_max(lane < nd ? (double)Hg[(int64_t)lane * np + lane] : 0.0));
+    const double tol = 1e-9 * scale;
+    double tyi[2];  // R_r y_i
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int r = lane + 64 * k;
+        tyi[k] = r < nr ? row_dot<NP>(S, ls, nd, r, S.y) : 0.0;
+    }
+    for (int rd = 0; rd < XO_ROUNDS; ++rd) {
+        // weights of K_A and the correction's right-hand side: rhs - K_A y_i = -c - Hy y_i + R' (w (bd - R y_i))
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = lane + 64 * k;
+            if (r < P.rmax) {
+                const double w = r < nr ? ((fl[k] & 1) ? rho : (fl[k] & 2) ? 1.0 : 0.0) : 0.0;
+                S.wh[r] = w;
+                S.q[r] = r < nr ? w * (bd[k] - tyi[k]) : 0.0;
+            }
+        }
+        LMPC_SYNC();
+        form_K(P, S, nr, nd, Hg, lane);
+        chol_floor<NP>(S, ls, nd, lane);
+        double rr = 0.0;
+        if (lane < nd) rr = -S.c[lane] - hy_dot<NP>(P, Hg, S.y, nd, lane) + rt_dot(S, ls, nr, S.q, lane);
+        const double d0 = chol_solve<NP>(S, ls, nd, rr, S.vb, lane);
+        const double y0 = lane < nd ? yi + d0 : 0.0;
+        if (lane < np) S.dy[lane] = y0;
+        const unsigned long long m0 = __ballot(fl[0] & 1), m1 = __ballot(fl[1] & 1);
+        const int na = __popcll(m0) + __popcll(m1);
+        if (na > np || na > 64) return false;
+        LMPC_SYNC();
+        // T rows a = K_A^-1 R_{r_a}' (global scratch); active row indices in S.rt
+        unsigned long long w0 = m0, w1 = m1;
+        for (int a = 0; a < na; ++a) {
+            int r;
+            if (w0) {
+                r = __ffsll((long long)w0) - 1;
+                w0 &= w0 - 1;
+            } else {
+                r = 64 + __ffsll((long long)w1) - 1;
+                w1 &= w1 - 1;
+            }
+            r = uni(r);
+            const double rj = lane < nd ? (double)S.R[r * ls + lane] : 0.0;
+            const double t = chol_solve<NP>(S, ls, nd, rj, S.vb, lane);
+            if (lane < np) Tg[(int64_t)a * np + lane] = lane < nd ? t : 0.0;
+            if (lane == 0) S.rt[a] = r;
+        }
+        LMPC_GSYNC();  // T and the row list visible to every lane
+        double lam = 0.0, y = y0;
+        if (na > 0) {
+            // Schur complement Sm = R_A T' (symmetric): lane b < na holds T row b, forms row b of Sm into S.KL (K_A's
+            // factor is no longer needed) and e_b = R_{r_b} y0 - h_{r_b}
+            const bool lb = lane < na;
+            const int nt = nd_tiles(nd);
+            double tb[NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) tb[j] = 0.0;
+            if (lb) {
+#pragma unroll
+                for (int J = 0; J < NP / 16; ++J)
+                    if (J < nt) {
+#pragma unroll
+                        for (int j = 16 * J; j < 16 * J + 16; ++j) tb[j] = Tg[(int64_t)lane * np + j];
+                    }
+            }
+            for (int a = 0; a < na; ++a) {
+                const int ra = uni(S.rt[a]);
+                double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+                for (int J = 0; J < NP / 16; ++J)
+                    if (J < nt) {
+#pragma unroll
+                        for (int j = 16 * J; j < 16 * J + 16; j += 2) {
+                            v0 = fma(S.R[ra * ls + j], tb[j], v0);
+                            v1 = fma(S.R[ra * ls + j + 1], tb[j + 1], v1);
+                        }
+                    }
+                if (lb) S.KL[lane * ls + a] = v0 + v1;
+            }
+            double e = 0.0;
+            if (lb) {
+                const int rb = S.rt[lane];
+                e = row_dot<NP>(S, ls, nd, rb, S.dy) - S.t[rb];
+            }
+            const int nts = nd_tiles(na);  // padding columns na..16 nts - 1 zero (chol_floor loads whole tiles)
+            if (lb)
+                for (int j = na; j < 16 * nts; ++j) S.KL[lane * ls + j] = 0.0;
+            LMPC_SYNC();
+            chol_floor<NP>(S, ls, na, lane);
+            lam = chol_solve<NP>(S, ls, na, e, S.vb, lane);  // lane a: lambda_a
+            for (int a = 0; a < na; ++a) {
+                const double la = readlane_f64(lam, a);
+                if (lane < nd) y = fma(-la, Tg[(int64_t)a * np + lane], y);
+            }
+            if (lane < np) S.dy[lane] = lane < nd ? y : 0.0;
+            LMPC_SYNC();
+        }
+        // verification, and the repair of the classification
+        double t[2];
+        bool flip = false;
+        double vin = -INFINITY;  // most violated inactive frozen row
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = lane + 64 * k;
+            t[k] = 0.0;
+            if (r < nr) {
+                t[k] = row_dot<NP>(S, ls, nd, r, S.dy) - bd[k];
+                if (r < p) {
+                    if (!(fl[k] & 1)) vin = fmax(vin, t[k]);
+                } else {
+                    const bool fk = (fl[k] & 2) ? !(t[k] >= -tol) : !(t[k] <= tol);
+                    flip |= fk;
+                }
+            }
+        }
+        const double lmin = wave_min(lane < na ? lam : INFINITY);
+        const double vmax = wave_max(vin);
+        const bool anyflip = __any(flip);
+        if (!(lmin == lmin) || !(vmax == vmax)) return false;  // non-finite
+        bool changed = false;
+        if (lmin < -tol) {  // the most negative multiplier's row leaves the active set
+            const int a = __ffsll((long long)__ballot(lane < na && lam == lmin)) - 1;
+            const int r = uni(S.rt[a]);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (lane + 64 * k == r) fl[k] &= ~1;
+            changed = true;
+        }
+        if (vmax > tol) {  // the most violated inactive frozen row enters
+            int r = -1;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const unsigned long long b = __ballot(lane + 64 * k < p && !(fl[k] & 1) && t[k] == vmax);
+                if (r < 0 && b) r = 64 * k + __ffsll((long long)b) - 1;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (lane + 64 * k == r) fl[k] |= 1;
+            changed = true;
+        }
+        if (anyflip) {  // own rows to the side they land on
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                if (r >= p && r < nr && ((fl[k] & 2) ? !(t[k] >= -tol) : !(t[k] <= tol))) fl[k] ^= 2;
+            }
+            changed = true;
+        }
+        if (changed) continue;
+        // stationarity: Hy y + c + R'z, z = lambda on the active frozen rows, R y - g on the violated own rows
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = lane + 64 * k;
+            if (r < P.rmax) S.q[r] = (r < nr && (fl[k] & 2)) ? t[k] : 0.0;
+        }
+        LMPC_SYNC();
+        if (lane < na) S.q[S.rt[lane]] = lam;
+        LMPC_SYNC();
+        double st = 0.0;
+        if (lane < nd) st = hy_dot<NP>(P, Hg, S.dy, nd, lane) + S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
+        if (__any(!(fabs(st) <= tol) || !(y == y))) return false;  // NaN fails every comparison
+        if (lane < np) S.y[lane] = lane < nd ? y : 0.0;
+        LMPC_SYNC();
+        return true;
+    }
+    return false;
+}
+
 // Interior-point state of the level's rows, slot k = row lane + 64 k (rows < nr = p + s, own rows r >= p).
 struct Rows {
     double s1[2], z1[2], v[2];  // own rows: -v <= 0 with slack s1
@@ -736,6 +941,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     gdouble* zbuf[2] = {(gdouble*)(scratch + (int64_t)b * P.scratch_len),
                         (gdouble*)(scratch + (int64_t)b * P.scratch_len + (int64_t)P.n * P.np)};
     gdouble* Hg = (gdouble*)(scratch + (int64_t)b * P.scratch_len + 2 * (int64_t)P.n * P.np);
+    gdouble* Tg = Hg + (int64_t)P.np * P.np;  // crossover: K_A^-1 R_A' rows (np x np)
     gdouble* wo = (gdouble*)(wout + (int64_t)b * P.slack_len);
     int zc = 0;
     // a non-finite record entry reaches the first residuals of its level (the residual maximum propagates NaN);
@@ -816,7 +1022,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         // ---- interior point --------------------------------------------------------------------------
         int it = 0;
         bool numstop = false;  // left on a non-finite Newton direction
-        double mu_last = 0.0;
+        bool clean = false;    // stopped on the clean criterion (complementarity and residuals within tolerance)
+        double mu_last = 0.0, res_last = 0.0;
         for (;; ++it) {
             // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
             double rp1[2], rpg[2], rdv[2];
@@ -851,6 +1058,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
             mu_last = mu;
             res = wave_reduce<OpNanMax>(res);
+            res_last = res;
             HSTAMP(3);
             if (!(isfinite(mu) && isfinite(res))) {
                 nonfin = true;
@@ -859,8 +1067,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             // converged; or degenerate (rows whose slack and multiplier both vanish): complementarity 1e3 below
             // its tolerance while the dual residual stalls within 1e3 of its own, where the huge weights z/s
             // of those rows leave the Newton directions no more accurate than the iterate already is
-            if ((mu <= P.tol_mu * scale && res <= P.tol_res * scale) ||
-                (mu <= 1e-3 * P.tol_mu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter)
+            clean = mu <= P.tol_mu * scale && res <= P.tol_res * scale;
+            if (clean || (mu <= 1e-3 * P.tol_mu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter)
                 break;
             // weights and K = Hy + R' diag(wh) R
             double w1[2], wg[2], dl[2], is1[2], isg[2], idl[2];  // weights and the reciprocals both Newton
@@ -995,8 +1203,29 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             HQSUB(6);
             HSTAMP(6);
         }
-        if (it >= P.max_iter || (numstop && mu_last > 1e3 * P.tol_mu * scale)) st = 1;
-        if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it;
+        // the exact crossover on the identified active set, taken when it verifies: the clean stop's residual
+        // tolerance (1e-7 of the scale by default) is far looser than the active-set answer
+        bool exact = false;
+        int xo = 0;  // iteration word bits 16-17: 1 crossover tried, 2 verified and taken
+        if (P.crossover && !nonfin && nr > 0 && nd > 0) {
+            int fl[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                fl[k] = 0;
+                if (r < p) fl[k] = W.zg[k] > W.sg[k] ? 1 : 0;
+                else if (r < nr) fl[k] = W.zg[k] > W.sg[k] ? 2 : 0;
+            }
+            exact = crossover<NP>(P, S, p, nr, nd, W.bd[0], W.bd[1], fl[0], fl[1], scale, Hg, Tg, lane);
+            xo = exact ? 3 : 1;
+        }
+        exact = exact || clean;
+        // LMPC_QP_CONVERGED: the clean stop, a verified crossover, or -- documented in lmpc_hoqp.h -- the relaxed
+        // degenerate stop (complementarity 1e3 below its tolerance, residuals within 1e3 of theirs); a level left on
+        // the iteration cap or on a non-finite direction short of that reports LMPC_QP_MAX_ITER
+        const bool relaxed = mu_last <= 1e-3 * P.tol_mu * scale && res_last <= 1e3 * P.tol_res * scale;
+        if (!exact && (it >= P.max_iter || (numstop && !relaxed))) st = 1;
+        if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16);
         // ---- outputs: w_l = max(0, D_l Z y - g) for the final y, x += Z y ------------------------------
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -1020,7 +1249,12 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         }
         p = nr;
         HSTAMP(7);
-        if (nonfin) break;
+        if (nonfin) {
+            // the levels below are not solved: their iteration counts read 0
+            if (iters && lane == 0)
+                for (int l2 = l + 1; l2 < P.L; ++l2) iters[(int64_t)b * P.L + l2] = 0;
+            break;
+        }
     }
     HSTAMP_FLUSH(b);
     // non-finite result or residuals: zeros, LMPC_QP_NAN

@@ -24,7 +24,8 @@ struct HoqpDev {
     int kmax;                // LDS rows of K / G: max(np, max m)
     int max_iter;
     double tol_mu, tol_res;
-    int64_t scratch_len;     // doubles of global scratch per instance: Z, Z', A'A (np x np each, padded)
+    int crossover;           // 1: exact active-set crossover after each level's interior point (lmpc_hoqp.hip)
+    int64_t scratch_len;     // doubles of global scratch per instance: Z, Z' (n x np), Hy and the crossover's T (np x np)
 };
 
 __host__ __device__ inline int hq_ls(const HoqpDev& P) { return P.np + 1; }  // LDS row stride (odd: rows fall on different banks)

@@ -1449,7 +1449,11 @@ hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* con
     // device has SIMDs (up to one QP per SIMD the lone-wave instance, free of spills, is faster); H <= 16
     // only: the LS = 2 state spills too much at 256 registers (measured at H = 20, 5 QPs per CU: 22 %
     // slower than 4 at one wave per SIMD).  Same arithmetic, so the choice never changes a result bit.
+#ifdef LMPC_AB_NO_W2  // diagnostic variant (tools/ab_bench.sh): the lone-wave instance only
+    const bool w2 = false;
+#else
     const bool w2 = !two && 5 * lds_bytes(prm.H, normals != nullptr) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
+#endif
 #define LMPC_LAUNCH(LS_, T_, W_) \
     launch_variant<LS_, T_, W_>(prm, rec, contact, normals, batch, grf, status, iters, scratch, done, stream)
     if (normals) {

@@ -126,9 +126,11 @@ class HoqpBatch:
         except Exception:
             pass
 
-    def set_options(self, max_iter=None, tol_mu=None, tol_res=None):
+    def set_options(self, max_iter=None, tol_mu=None, tol_res=None, crossover=None):
         o = N.LmpcHoqpOptions()
         self._L.lmpc_hoqp_options_default(ctypes.byref(o))
+        if crossover is not None:
+            o.crossover = int(crossover)
         if max_iter is not None:
             o.max_iter = max_iter
         if tol_mu is not None:

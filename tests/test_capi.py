@@ -92,7 +92,7 @@ def test_eigen_signature_header_compiles_with_reference_call_sites():
     (tests/cpp/eigen_dropin_test.cpp, against test stand-ins of Eigen and the reference headers)."""
     from legged_mpc_control_amd import build as B
 
-    exe = B.build_cpp_eigen_test(force=True)
+    exe = B.build_cpp_eigen_test()
     assert os.path.exists(exe) and os.access(exe, os.X_OK)
     src = open(os.path.join(ROOT, "tests", "cpp", "eigen_dropin_test.cpp")).read()
     # the reference's own lines (ConvexMpc.cpp:13-14,70-72), verbatim

@@ -65,7 +65,7 @@ def test_dims_record_layout_and_limits():
     assert lib.lmpc_hoqp_record_len(ctypes.byref(big)) == -1
     o = N.LmpcHoqpOptions()
     lib.lmpc_hoqp_options_default(ctypes.byref(o))
-    assert o.max_iter == 60 and o.tol_mu == 1e-13 and o.tol_res == 1e-7
+    assert o.max_iter == 60 and o.tol_mu == 1e-13 and o.tol_res == 1e-7 and o.crossover == 1
 
 
 def test_create_and_solve_reject_bad_arguments_without_gpu():

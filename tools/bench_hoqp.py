@@ -119,7 +119,9 @@ def main():
     x = d_x.cpu().numpy()
     w = d_w.cpu().numpy()[:, :solver.slack_len]
     st = d_st.cpu().numpy()
-    it = d_it.cpu().numpy()
+    it_word = d_it.cpu().numpy()
+    it = it_word & 0xFFFF          # interior-point iterations; bits 16-17: crossover tried (1) / verified (3)
+    xo = it_word >> 16
     # work model: measured iterations per level, null-space dimensions from the instances themselves
     nds = [null_dims(c) for c in chains[:128]]
     flop = 0.0
@@ -213,6 +215,7 @@ def main():
             "status": {"converged": int(stats[0]), "max_iter": int(stats[1]), "nan": int(stats[2])},
             "ipm_iters_per_level_mean": [float(v) for v in it.mean(axis=0)],
             "ipm_iters_per_level_max": [int(v) for v in it.max(axis=0)],
+            "crossover_verified_per_level": [float(v) for v in (xo == 3).mean(axis=0)],
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -86,6 +86,83 @@ def polish(Hy, c, P, h, Dz, g, y_ipm, s2, z2, s3, z3, scale, rounds=3):
 
 
 POLISH_STATS = []
+XO_STATS = []
+
+
+def crossover(Hy, c, P, h, Dz, g, y_ipm, s1, z1, s2, z2, scale, rounds=int(os.environ.get("XO_ROUNDS", 6))):
+    """lmpc_hoqp.hip crossover(): frozen rows with z > s held exactly (Schur complement on the active rows), own
+    rows with v > 0 (s1 > z1) as 1/2 (d y - g)^2; the classification repaired for a few rounds (violated frozen rows
+    in, negative multipliers out, own rows moved to the side they land on); kept only if it verifies."""
+    p, s = P.shape[0], Dz.shape[0]
+    fa = (z2 > s2) if p else np.zeros(0, bool)
+    ob = (z1 > s1) if s else np.zeros(0, bool)  # called with the row constraint's (s3, z3): violated where z3 > s3
+    tol = 1e-9 * scale
+    for rd in range(rounds):
+        RA = P[fa] if p else np.zeros((0, len(c)))
+        na = RA.shape[0]
+        K = Hy + (Dz[ob].T @ Dz[ob] if s else 0)
+        # augmented-Lagrangian term rho R_A'R_A: the same constrained optimum (R_A y = h_A there), and K stays
+        # invertible where only the active rows bind (Hy is singular along ker G)
+        rho = float(os.environ.get("XO_RHO", 0.0)) * max(1.0, float(np.max(np.diag(K))))
+        K = K + rho * RA.T @ RA
+        L = chol_floor(K)
+        # a correction from the interior-point iterate: along directions where K is singular to rounding (flat
+        # objective) the floored pivots keep the iterate's components, which satisfy the inactive rows
+        rhs = -c + (Dz[ob].T @ g[ob] if s else 0) + rho * RA.T @ (h[fa] if p else np.zeros(0))
+        y0 = y_ipm + chol_solve(L, rhs - K @ y_ipm)
+        y = y0
+        lam = np.zeros(0)
+        if na:
+            T = np.stack([chol_solve(L, RA[a]) for a in range(na)])  # rows K^-1 R_a'
+            Sm = RA @ T.T
+            e = RA @ y0 - h[fa]
+            Ls = chol_floor(Sm)
+            lam = chol_solve(Ls, e)
+            y = y0 - T.T @ lam
+        changed = False
+        vmax = 0.0
+        if os.environ.get("XO_VERBOSE"):
+            tp_ = (P @ y - h) if p else np.zeros(0)
+            t_ = (Dz @ y - g) if s else np.zeros(0)
+            print(f"    xo rd {rd}: na {na} ob {int(ob.sum()) if s else 0} min lam {lam.min() if na else 0:.2e} "
+                  f"frozen-inactive max {np.max(tp_[~fa]) if p and (~fa).any() else 0:.2e} "
+                  f"own ob min {np.min(t_[ob]) if s and ob.any() else 0:.2e} own !ob max {np.max(t_[~ob]) if s and (~ob).any() else 0:.2e}"
+                  f" |y-yipm| {np.max(np.abs(y - y_ipm)):.2e}")
+        if na and np.any(lam < -tol):
+            idx = np.nonzero(fa)[0]
+            fa[idx[np.argmin(lam)]] = False
+            vmax = max(vmax, -lam.min())
+            changed = True
+        if p:
+            tp = P @ y - h
+            bad = (~fa) & (tp > tol)
+            if np.any(bad):
+                k = np.argmax(np.where(bad, tp, -np.inf))
+                fa[k] = True
+                vmax = max(vmax, tp[k])
+                changed = True
+        if s:
+            t = Dz @ y - g
+            flip = (ob & (t < -tol)) | ((~ob) & (t > tol))
+            if np.any(flip):
+                ob = ob ^ flip
+                vmax = max(vmax, np.max(np.abs(t[flip])))
+                changed = True
+        if not changed:
+            # stationarity residual of the level's KKT system at the crossover point (diagnostic)
+            lf = np.zeros(p)
+            if na:
+                lf[fa] = lam
+            z3 = np.maximum(0.0, Dz @ y - g) if s else np.zeros(0)
+            st = Hy @ y + c + (P.T @ lf if p else 0) + (Dz.T @ z3 if s else 0)
+            sres = float(np.max(np.abs(st))) / scale
+            if sres > 1e-9:
+                XO_STATS.append((False, rd, sres))
+                return y_ipm
+            XO_STATS.append((True, rd, int(fa.sum()) if p else 0, int(ob.sum()) if s else 0, sres))
+            return y
+    XO_STATS.append((False, rounds, vmax / scale))
+    return y_ipm
 
 
 def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1e-13)), frac=0.99, stats=None):
@@ -174,6 +251,8 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
         stats.append(it)
     if os.environ.get("POLISH"):
         y = polish(Hy, c, P, h, Dz, g, y, s2, z2, s3, z3, scale)
+    if os.environ.get("EXACT"):
+        y = crossover(Hy, c, P, h, Dz, g, y, s3, z3, s2, z2, scale)
     if s and os.environ.get("VEXACT"):
         v = np.maximum(0.0, Dz @ y - g)
     if os.environ.get("VERBOSE"):
