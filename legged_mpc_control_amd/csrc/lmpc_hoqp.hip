@@ -730,6 +730,7 @@ __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS
 // (uniform); on success S.y holds the exact y.  The reference solves each level exactly with qpOASES
 // (HoQp.cpp:158-174), an active-set method: this makes the degenerate levels exact too.
 constexpr int XO_ROUNDS = 6;
+constexpr double HQ_HFLOOR = 1e-10;  // interior-point margin on exactly tight frozen rows (kernel, below)
 template <int NP>
 __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS& S_, int p, int nr, int nd, double bd0,
                                                     double bd1, int fl0, int fl1, double scale, const gdouble* Hg,
@@ -1017,6 +1018,17 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         }
         LMPC_SYNC();
         const double scale = 1.0 + fmax(wave_max(lane < nd ? fabs(S.c[lane]) : 0.0), wave_max(bmax));
+        // A frozen row the crossover of a level above left exactly tight has h = 0 up to rounding (or one ulp
+        // below).  Several such rows around a vertex leave the level's feasible set without an interior, and the
+        // interior point then stalls (slacks to the bottom of the range, multipliers unbounded).  With the
+        // crossover on, the interior point sees those bounds raised to HQ_HFLOOR of the scale -- the margin a
+        // level-above iterate would have left -- and the crossover then solves with the true bounds.
+        const double hb_true[2] = {W.bd[0], W.bd[1]};
+        if (P.crossover) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (lane + 64 * k < p) W.bd[k] = fmax(W.bd[k], HQ_HFLOOR * scale);
+        }
         const double mc = (double)(p + 2 * s);
         HSTAMP(2);
         // ---- interior point --------------------------------------------------------------------------
@@ -1216,7 +1228,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 if (r < p) fl[k] = W.zg[k] > W.sg[k] ? 1 : 0;
                 else if (r < nr) fl[k] = W.zg[k] > W.sg[k] ? 2 : 0;
             }
-            exact = crossover<NP>(P, S, p, nr, nd, W.bd[0], W.bd[1], fl[0], fl[1], scale, Hg, Tg, lane);
+            exact = crossover<NP>(P, S, p, nr, nd, hb_true[0], hb_true[1], fl[0], fl[1], scale, Hg, Tg, lane);
             xo = exact ? 3 : 1;
         }
         exact = exact || clean;

@@ -183,6 +183,13 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
     z1, z2, z3 = z0 * np.ones(s), z0 * np.ones(p), z0 * np.ones(s)
     scale = 1.0 + max(np.max(np.abs(c)) if nd else 0.0, np.max(np.abs(h)) if p else 0.0,
                       np.max(np.abs(g)) if s else 0.0)
+    # frozen rows the levels above left exactly tight (h ~ 0 after their crossover): the interior point gets a
+    # margin of HFLOOR of the scale so its feasible set keeps an interior; the crossover uses the true bound
+    h_true = h
+    hf = float(os.environ.get("HFLOOR", 0.0))
+    if p and hf:
+        h = np.maximum(h, hf * scale)
+        s2 = np.maximum(h - P @ y, floor)
     it = 0
     for it in range(max_iter):
         # residuals: r_d = H x + c + C'z, r_p = C x + sigma - d
@@ -252,11 +259,16 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
     if os.environ.get("POLISH"):
         y = polish(Hy, c, P, h, Dz, g, y, s2, z2, s3, z3, scale)
     if os.environ.get("EXACT"):
-        y = crossover(Hy, c, P, h, Dz, g, y, s3, z3, s2, z2, scale)
+        y = crossover(Hy, c, P, h_true, Dz, g, y, s3, z3, s2, z2, scale)
     if s and os.environ.get("VEXACT"):
         v = np.maximum(0.0, Dz @ y - g)
     if os.environ.get("VERBOSE"):
         print(f"    ipm it {it} mu {mu:.1e} res {res:.1e} scale {scale:.1e}")
+        if os.environ.get("VERBOSE") == "2":
+            print(f"      |rdy| {np.max(np.abs(rdy)) if nd else 0:.1e} |rdv| {np.max(np.abs(rdv)) if s else 0:.1e} "
+                  f"|rp1| {np.max(np.abs(rp1)) if s else 0:.1e} |rp2| {np.max(np.abs(rp2)) if p else 0:.1e} "
+                  f"|rp3| {np.max(np.abs(rp3)) if s else 0:.1e} max z2 {np.max(z2) if p else 0:.1e} "
+                  f"min s2 {np.min(s2) if p else 0:.1e}")
     return y, v, it
 
 
