@@ -137,20 +137,24 @@ __device__ __forceinline__ const double* cons_row(const HoqpDev& P, const double
     return lev_d(P, rec, lev) + (int64_t)idx * P.n;
 }
 
-// C[rows][0..np) = X Z on the matrix cores; X row r = xrow(r) (global, n entries), Z global n x np
-// (columns nd..np-1 zero).  A[m][k] comes from lane 16k+m, B[k][n] from lane 16k+n, C element (4i+g, c)
-// lands in register i of lane 16g+c.
+// C[rows][0..16 nt) = X Z on the matrix cores; X row r = xrow(r) (global, n entries), Z global n x np, of which
+// only the nt column tiles that cover the level's nd coordinates are read (columns nd..16 nt - 1 zero; Z == nullptr:
+// Z = I, generated, as long as no level above had equalities).  A[m][k] comes from lane 16k+m, B[k][n] from lane
+// 16k+n, C element (4i+g, c) lands in register i of lane 16g+c.  Columns 16 nt.. of C are not written.
 template <int NP, class RowFn>
-__device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, const gdouble* Z, ldouble* C, int ldc,
-                                        int lane) {
+__device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, const gdouble* Z, int nt, ldouble* C,
+                                        int ldc, int lane) {
     constexpr int KC = NP / 4, NT = NP / 16;  // k chunks of 4, column tiles
     const int kq = lane >> 4, mm = lane & 15;
-    double bz[KC][NT];  // this lane's B operands for every chunk and tile, loaded once for all row tiles
+    double bz[KC][NT];  // this lane's B operands for every chunk and live tile, loaded once for all row tiles
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
         const int k = 4 * c + kq;
 #pragma unroll
-        for (int J = 0; J < NT; ++J) bz[c][J] = k < P.n ? Z[(int64_t)k * P.np + 16 * J + mm] : 0.0;
+        for (int J = 0; J < NT; ++J) {
+            bz[c][J] = 0.0;
+            if (J < nt && k < P.n) bz[c][J] = Z ? (double)Z[(int64_t)k * P.np + 16 * J + mm] : (k == 16 * J + mm ? 1.0 : 0.0);
+        }
     }
     for (int I = 0; I * 16 < rows; ++I) {
         const double* xr = (16 * I + mm < rows) ? xrow(16 * I + mm) : nullptr;
@@ -166,13 +170,16 @@ __device__ __forceinline__ void gemm_xz(const HoqpDev& P, RowFn xrow, int rows, 
 #pragma unroll
         for (int c = 0; c < KC; ++c)
 #pragma unroll
-            for (int J = 0; J < NT; ++J) acc[J] = MFMA64(a[c], bz[c][J], acc[J]);
+            for (int J = 0; J < NT; ++J)
+                if (J < nt) acc[J] = MFMA64(a[c], bz[c][J], acc[J]);
 #pragma unroll
         for (int J = 0; J < NT; ++J)
+            if (J < nt) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = 16 * I + 4 * i + kq;
-                if (row < rows) C[row * ldc + 16 * J + mm] = acc[J][i];
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * I + 4 * i + kq;
+                    if (row < rows) C[row * ldc + 16 * J + mm] = acc[J][i];
+                }
             }
     }
 }
@@ -568,6 +575,7 @@ __device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P_, con
     if (lane < nd) S.rt[S.qp[lane]] = lane;
     LMPC_SYNC();
     const int kq = lane >> 4, mm = lane & 15;
+    const int ntk = nd_tiles(dimker);  // Z' column tiles the next level reads (columns dimker..16 ntk - 1 zero)
     for (int I = 0; I * 16 < P.n; ++I) {
         const int zrow = 16 * I + mm;
         d4 acc[4];
@@ -575,11 +583,12 @@ __device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P_, con
         for (int J = 0; J < 4; ++J) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
         for (int k0 = 0; k0 < nd; k0 += 4) {
             const int j = k0 + kq;
-            const double a = (zrow < P.n && j < nd) ? Z[(int64_t)zrow * P.np + j] : 0.0;
+            const double a = (zrow < P.n && j < nd) ? (Z ? (double)Z[(int64_t)zrow * P.np + j] : (zrow == j ? 1.0 : 0.0))
+                                                    : 0.0;
             const int qi = j < nd ? S.rt[j] : -1;
 #pragma unroll
             for (int J = 0; J < 4; ++J)
-                if (J < P.nt) {
+                if (J < ntk) {
                     const int c = 16 * J + mm;
                     double bk = 0.0;
                     if (qi >= 0 && c < dimker) bk = qi < rank ? -S.KL[qi * ls + rank + c] : (qi - rank == c ? 1.0 : 0.0);
@@ -588,7 +597,7 @@ __device__ __attribute__((noinline)) int fullpivlu_kernel(const HoqpDev& P_, con
         }
 #pragma unroll
         for (int J = 0; J < 4; ++J)
-            if (J < P.nt) {
+            if (J < ntk) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int row = 16 * I + 4 * i + kq;
@@ -639,7 +648,7 @@ __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P_, const H
     for (int t = 0; t < 10; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     if (m > 0) {
         const double* A = lev_a(P, rec, l);
-        gemm_xz<NP>(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, S.KL, ls, lane);
+        gemm_xz<NP>(P, [&](int r) { return A + (int64_t)r * P.n; }, m, Z, nt, S.KL, ls, lane);
         if (lane < m) {
             double amx;
             S.vb[lane] = gdot(A + (int64_t)lane * P.n, S.x, P.n, amx) - lev_b(P, rec, l)[lane];
@@ -703,13 +712,14 @@ __device__ __attribute__((noinline)) void form_K(const HoqpDev& P_, const HS& S_
 // Constraint rows R = [D_stack; D_l] Z (rows 0..nr-1 of S.R).
 template <int NP>
 __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS& S_, const double* rec, int l, int p,
-                                                     int nr, const gdouble* Z, int lane) {
+                                                     int nr, const gdouble* Z, int nd, int lane) {
     const HS S = S_;
     const HoqpDev P = uniform(P_);
     l = uni(l);
     p = uni(p);
     nr = uni(nr);
-    gemm_xz<NP>(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, S.R, hq_ls(P), lane);
+    gemm_xz<NP>(P, [&](int r) { double f; return cons_row(P, rec, l, p, r, f); }, nr, Z, nd_tiles(uni(nd)), S.R,
+                hq_ls(P), lane);
 }
 
 // Exact crossover (round 3) after an interior point that stopped short of its clean criterion (degenerate
@@ -949,9 +959,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     // so does an overflow: zeros and LMPC_QP_NAN, as the MPC path returns zero forces for a NaN solve
     // (ConvexQPSolver.cpp:321-326)
     bool nonfin = false;
-    // Z = I, x = 0
-    if (lane < P.n)
-        for (int j = 0; j < P.np; ++j) zbuf[0][(int64_t)lane * P.np + j] = (j == lane) ? 1.0 : 0.0;
+    // x = 0; Z = I is generated, not stored, until the first level with equalities (zident)
+    bool zident = true;
     if (lane < P.np) S.x[lane] = 0.0;
     LMPC_GSYNC();
     int nd = P.n, p = 0, st = 0;
@@ -959,7 +968,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     HQSUB_DECL
     for (int l = 0; l < P.L; ++l) {
         const int m = P.m[l], s = P.s[l], nr = p + s;
-        const gdouble* Z = zbuf[zc];
+        const gdouble* Z = zident ? nullptr : zbuf[zc];
         // ---- setup: G = A Z into KL, A x - b, c = G'(A x - b), Hy = G'G + 1e-12 I ---------------
         level_setup<NP>(P, S, rec, l, nd, Z, Hg, lane);
         LMPC_GSYNC();
@@ -969,14 +978,18 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         if (m > 0) nd_next = fullpivlu_kernel(P, S, m, nd, Z, zbuf[zc ^ 1], lane);
         HSTAMP(1);
         // ---- constraint rows R = [D_stack; D_l] Z and their bounds -----------------------------------
-        build_rows<NP>(P, S, rec, l, p, nr, Z, lane);
+        build_rows<NP>(P, S, rec, l, p, nr, Z, nd, lane);
         // A higher level's row that lies in the span of the equalities fixed since (its projection D Z is zero
         // up to rounding) constrains no y: 0 <= h, with h at rounding level when the row was active.  It is
         // dropped (R row zeroed, h = 1) rather than left to make the level infeasible by one ulp.
         double zmax = 0.0;
-        if (lane < P.n)
-            for (int j = 0; j < nd; ++j) zmax = fmax(zmax, fabs(Z[(int64_t)lane * P.np + j]));
-        zmax = wave_max(zmax);
+        if (zident) {
+            zmax = 1.0;
+        } else {
+            if (lane < P.n)
+                for (int j = 0; j < nd; ++j) zmax = fmax(zmax, fabs(Z[(int64_t)lane * P.np + j]));
+            zmax = wave_max(zmax);
+        }
         LMPC_SYNC();
         Rows W;
         double bmax = 0.0;
@@ -1246,9 +1259,13 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         }
         double xn = 0.0;
         if (lane < P.n) {
-            const gdouble* zr = Z + (int64_t)lane * P.np;
             double a = S.x[lane];
-            for (int j = 0; j < nd; ++j) a = fma(zr[j], S.y[j], a);
+            if (zident) {
+                a += S.y[lane];
+            } else {
+                const gdouble* zr = Z + (int64_t)lane * P.np;
+                for (int j = 0; j < nd; ++j) a = fma(zr[j], S.y[j], a);
+            }
             xn = a;
             xout[((int64_t)b * P.L + l) * P.n + lane] = a;
         }
@@ -1256,7 +1273,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         if (lane < P.n) S.x[lane] = xn;
         LMPC_GSYNC();
         if (m > 0) {
-            zc ^= 1;
+            zc ^= 1;  // fullpivlu wrote Z' into zbuf[zc ^ 1]
+            zident = false;
             nd = nd_next;
         }
         p = nr;
