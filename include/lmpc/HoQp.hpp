@@ -11,7 +11,8 @@
 //
 // Each HoQp object solves the whole chain up to its level on the device (one launch, batch 1; the higher
 // levels' results are recomputed identically) -- the reference solves one qpOASES QProblem per object.
-// getStackedZMatrix() is not provided: the null-space basis stays on the device.
+// getStackedZMatrix() returns the device's basis after this level (lmpc_hoqp_solve_batch_z: Eigen's FullPivLU
+// kernel basis, restated on the device).
 #pragma once
 
 #include <algorithm>
@@ -132,6 +133,7 @@ public:
     Task getStackedTasks() const { return stacked_tasks_; }
     vector_t getStackedSlackSolutions() const { return stacked_slack_vars_; }
     vector_t getSolutions() const { return x_; }
+    matrix_t getStackedZMatrix() const { return stacked_z_; }  // HoQp.h:26-29
     size_t getSlackedNumVars() const { return (size_t)stacked_tasks_.d_.rows(); }
     int status() const { return status_; }  // LMPC_QP_* of the device solve (not in the reference)
 
@@ -167,6 +169,8 @@ private:
         }
         const int S = lmpc_hoqp_slack_len(&dims);
         std::vector<double> x((size_t)(dims.num_levels * n)), w((size_t)(S > 0 ? S : 1));
+        std::vector<double> z((size_t)(dims.num_levels * n * n));
+        std::vector<int32_t> zc((size_t)dims.num_levels);
         int32_t st = 0;
         Slot& slot = context(dims);
         int rc;
@@ -174,9 +178,9 @@ private:
             // a context's staging buffers and event are not thread-safe (lmpc_hoqp.h): same-shaped chains built
             // on several threads take turns on the shared context for the whole pack/solve/copy-out
             std::lock_guard<std::mutex> g(slot.mu);
-            rc = lmpc_hoqp_solve_batch(slot.ctx, rec.data(), 1, x.data(), w.data(), &st, nullptr);
+            rc = lmpc_hoqp_solve_batch_z(slot.ctx, rec.data(), 1, x.data(), w.data(), &st, nullptr, z.data(), zc.data());
         }
-        if (rc != LMPC_OK) throw std::runtime_error(std::string("lmpc_hoqp_solve_batch: ") + lmpc_strerror(rc));
+        if (rc != LMPC_OK) throw std::runtime_error(std::string("lmpc_hoqp_solve_batch_z: ") + lmpc_strerror(rc));
         status_ = st;
         const size_t last = chain.size() - 1;
         x_ = vector_t(n);
@@ -185,6 +189,10 @@ private:
         for (size_t l = 0; l <= last; ++l) ns += dims.ineq_rows[l];
         stacked_slack_vars_ = vector_t(ns);  // [w_0; ...; w_l], current level last (HoQp.cpp:176-182)
         for (int i = 0; i < ns; ++i) stacked_slack_vars_[i] = w[(size_t)i];
+        const long nz = zc[last];  // Z after this level: n x nz of the row-major n x n block
+        stacked_z_ = matrix_t(n, nz);
+        for (long i = 0; i < n; ++i)
+            for (long j = 0; j < nz; ++j) stacked_z_(i, j) = z[(last * n + (size_t)i) * n + (size_t)j];
     }
 
     // one device context per distinct shape, kept for the life of the process (the reference re-creates its
@@ -217,6 +225,7 @@ private:
     Task task_, stacked_tasks_;
     HoQpPtr higher_problem_;
     vector_t x_, stacked_slack_vars_;
+    matrix_t stacked_z_;
     int status_ = 0;
 };
 

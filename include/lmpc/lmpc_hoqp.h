@@ -99,6 +99,17 @@ int lmpc_hoqp_solve_device(lmpc_hoqp_ctx* ctx, const double* d_tasks, int batch,
                            int32_t* d_status, int32_t* d_iters, void* stream);
 int lmpc_hoqp_sync(lmpc_hoqp_ctx* ctx);
 
+/* Round 3: the same solves, also returning every level's getStackedZMatrix() (HoQp.h:26-29: the null-space basis
+ * the levels below work in, Z_{l+1} = Z_l ker(A_l Z_l) by Eigen's FullPivLU kernel basis, HoQp.cpp:147-156; Z_l
+ * itself for a level without equalities).  z [batch][num_levels][num_vars][num_vars] row-major: level l's basis
+ * in its first zcols[b][l] columns, the rest zero (a trivial kernel is Eigen's single zero column: zcols 1).
+ * zcols [batch][num_levels] may be NULL; z NULL = the calls above.  LMPC_QP_NAN chains: zeros, zcols 0.
+ * The host path allocates its staging for z on first use (max_batch x num_levels x num_vars^2 doubles). */
+int lmpc_hoqp_solve_batch_z(lmpc_hoqp_ctx* ctx, const double* tasks, int batch, double* x, double* slack,
+                            int32_t* status, int32_t* iters, double* z, int32_t* zcols);
+int lmpc_hoqp_solve_device_z(lmpc_hoqp_ctx* ctx, const double* d_tasks, int batch, double* d_x, double* d_slack,
+                             int32_t* d_status, int32_t* d_iters, double* d_z, int32_t* d_zcols, void* stream);
+
 /* ---- WBC task formulation (wbc.cpp:102-259), the step before the hierarchical QP ----------------------------
  * Per robot, the dynamics terms the reference takes from Pinocchio (wbc.cpp:59-91) and the task targets; the
  * output is one record of the WBC layout (lmpc_hoqp_dims_wbc, 4472 doubles): level 0 = [M, -J', -S'] x = -h

@@ -42,6 +42,7 @@ HOQP_SYMBOLS = (
     "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
     "lmpc_hoqp_lds_bytes", "lmpc_hoqp_create", "lmpc_hoqp_destroy", "lmpc_hoqp_set_options", "lmpc_hoqp_solve_batch",
     "lmpc_hoqp_solve_device", "lmpc_hoqp_sync", "lmpc_wbc_tasks", "lmpc_wbc_tasks_device",
+    "lmpc_hoqp_solve_batch_z", "lmpc_hoqp_solve_device_z",
 )
 HOQP_MAX_LEVELS = 4
 # include/lmpc/lmpc_multi.h: one process, several GPUs (liblmpc_multi.so, RCCL scatter / gather)
@@ -270,6 +271,10 @@ def lib():
         L.lmpc_hoqp_solve_batch.restype = ctypes.c_int
         L.lmpc_hoqp_solve_device.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, vp, vp]
         L.lmpc_hoqp_solve_device.restype = ctypes.c_int
+        L.lmpc_hoqp_solve_batch_z.argtypes = [vp, dp, ctypes.c_int, dp, dp, i32p, i32p, dp, i32p]
+        L.lmpc_hoqp_solve_batch_z.restype = ctypes.c_int
+        L.lmpc_hoqp_solve_device_z.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp]
+        L.lmpc_hoqp_solve_device_z.restype = ctypes.c_int
         L.lmpc_hoqp_sync.argtypes = [vp]
         L.lmpc_hoqp_sync.restype = ctypes.c_int
         L.lmpc_wbc_tasks.argtypes = [ctypes.POINTER(LmpcWbcInput), dp]

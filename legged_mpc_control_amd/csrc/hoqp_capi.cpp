@@ -13,7 +13,7 @@
 
 namespace lmpc {
 hipError_t launch_hoqp(const HoqpDev& P, const double* rec, int batch, double* x, double* w, int32_t* status,
-                       int32_t* iters, double* scratch, hipStream_t stream);
+                       int32_t* iters, double* zout, int32_t* zcols, double* scratch, hipStream_t stream);
 }
 
 struct lmpc_hoqp_ctx {
@@ -26,6 +26,8 @@ struct lmpc_hoqp_ctx {
     int32_t* d_st = nullptr;    // host path staging: status | iters
     double* d_scratch = nullptr;  // per-instance Z, Z', A'A, grown on demand
     size_t scratch_inst = 0;
+    double* d_z = nullptr;      // host path staging: stacked Z matrices + column counts (allocated on first use)
+    int32_t* d_zc = nullptr;
     hipEvent_t ev = nullptr;    // orders launches that share d_scratch across streams
     hipStream_t ev_stream = nullptr;
     bool ev_live = false;
@@ -121,11 +123,11 @@ bool stream_ok(hipStream_t s, int dev) {
 }
 
 hipError_t launch(lmpc_hoqp_ctx* c, const double* rec, int batch, double* x, double* w, int32_t* st, int32_t* it,
-                  hipStream_t s) {
+                  double* z, int32_t* zc, hipStream_t s) {
     hipError_t e = ensure_scratch(c, batch);
     if (e != hipSuccess) return e;
     if (c->ev_live && c->ev_stream != s && (e = hipStreamWaitEvent(s, c->ev, 0)) != hipSuccess) return e;
-    e = lmpc::launch_hoqp(c->P, rec, batch, x, w, st, it, c->d_scratch, s);
+    e = lmpc::launch_hoqp(c->P, rec, batch, x, w, st, it, z, zc, c->d_scratch, s);
     if (e != hipSuccess) return e;
     e = hipEventRecord(c->ev, s);
     c->ev_stream = s;
@@ -216,6 +218,8 @@ void lmpc_hoqp_destroy(lmpc_hoqp_ctx* c) {
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_st);
     (void)hipFree(c->d_scratch);
+    (void)hipFree(c->d_z);
+    (void)hipFree(c->d_zc);
     if (c->ev) (void)hipEventDestroy(c->ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -232,14 +236,23 @@ int lmpc_hoqp_set_options(lmpc_hoqp_ctx* c, const lmpc_hoqp_options* o) {
     return LMPC_OK;
 }
 
-int lmpc_hoqp_solve_batch(lmpc_hoqp_ctx* c, const double* tasks, int batch, double* x, double* slack,
-                          int32_t* status, int32_t* iters) {
+int lmpc_hoqp_solve_batch_z(lmpc_hoqp_ctx* c, const double* tasks, int batch, double* x, double* slack,
+                            int32_t* status, int32_t* iters, double* z, int32_t* zcols) {
     if (!c || batch < 0 || batch > c->max_batch) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
     if (!tasks || !x || (!slack && c->P.slack_len > 0)) return LMPC_ERR_ARG;
     DeviceScope scope(c->device);
     if (!scope.ok) return LMPC_ERR_DEVICE;
     const size_t nx = (size_t)batch * c->P.L * c->P.n, nw = (size_t)batch * c->P.slack_len;
+    const size_t nz = (size_t)c->max_batch * c->P.L * c->P.n * c->P.n;
+    if (z && !c->d_z) {  // staging for the stacked Z matrices, on first use (max_batch x levels x n x n)
+        if (hipMalloc(&c->d_z, nz * sizeof(double)) != hipSuccess ||
+            hipMalloc(&c->d_zc, (size_t)c->max_batch * c->P.L * sizeof(int32_t)) != hipSuccess) {
+            (void)hipFree(c->d_z);
+            c->d_z = nullptr;
+            return LMPC_ERR_ALLOC;
+        }
+    }
     double* d_x = c->d_out;
     double* d_w = c->d_out + nx;
     int32_t* d_status = c->d_st;
@@ -248,28 +261,47 @@ int lmpc_hoqp_solve_batch(lmpc_hoqp_ctx* c, const double* tasks, int batch, doub
     if (hipMemcpyAsync(c->d_rec, tasks, (size_t)batch * c->P.rec_len * sizeof(double), hipMemcpyHostToDevice, s) !=
         hipSuccess)
         return LMPC_ERR_DEVICE;
-    if (launch(c, c->d_rec, batch, d_x, d_w, d_status, d_iters, s) != hipSuccess) return LMPC_ERR_LAUNCH;
+    if (launch(c, c->d_rec, batch, d_x, d_w, d_status, d_iters, z ? c->d_z : nullptr, z ? c->d_zc : nullptr, s) !=
+        hipSuccess)
+        return LMPC_ERR_LAUNCH;
     bool ok = hipMemcpyAsync(x, d_x, nx * sizeof(double), hipMemcpyDeviceToHost, s) == hipSuccess;
     if (nw) ok = ok && hipMemcpyAsync(slack, d_w, nw * sizeof(double), hipMemcpyDeviceToHost, s) == hipSuccess;
     if (status) ok = ok && hipMemcpyAsync(status, d_status, batch * sizeof(int32_t), hipMemcpyDeviceToHost, s) == hipSuccess;
     if (iters)
         ok = ok && hipMemcpyAsync(iters, d_iters, (size_t)batch * c->P.L * sizeof(int32_t), hipMemcpyDeviceToHost, s) ==
                        hipSuccess;
+    if (z)
+        ok = ok && hipMemcpyAsync(z, c->d_z, (size_t)batch * c->P.L * c->P.n * c->P.n * sizeof(double),
+                                  hipMemcpyDeviceToHost, s) == hipSuccess;
+    if (z && zcols)
+        ok = ok && hipMemcpyAsync(zcols, c->d_zc, (size_t)batch * c->P.L * sizeof(int32_t), hipMemcpyDeviceToHost, s) ==
+                       hipSuccess;
     ok = ok && hipStreamSynchronize(s) == hipSuccess;
     return ok ? LMPC_OK : LMPC_ERR_DEVICE;
 }
 
-int lmpc_hoqp_solve_device(lmpc_hoqp_ctx* c, const double* d_tasks, int batch, double* d_x, double* d_slack,
-                           int32_t* d_status, int32_t* d_iters, void* stream) {
+int lmpc_hoqp_solve_batch(lmpc_hoqp_ctx* c, const double* tasks, int batch, double* x, double* slack,
+                          int32_t* status, int32_t* iters) {
+    return lmpc_hoqp_solve_batch_z(c, tasks, batch, x, slack, status, iters, nullptr, nullptr);
+}
+
+int lmpc_hoqp_solve_device_z(lmpc_hoqp_ctx* c, const double* d_tasks, int batch, double* d_x, double* d_slack,
+                             int32_t* d_status, int32_t* d_iters, double* d_z, int32_t* d_zcols, void* stream) {
     if (!c || batch < 0) return LMPC_ERR_ARG;
     if (batch == 0) return LMPC_OK;
-    if (!d_tasks || !d_x || (!d_slack && c->P.slack_len > 0)) return LMPC_ERR_ARG;
+    if (!d_tasks || !d_x || (!d_slack && c->P.slack_len > 0) || (d_zcols && !d_z)) return LMPC_ERR_ARG;
     DeviceScope scope(c->device);
     if (!scope.ok) return LMPC_ERR_DEVICE;
     hipStream_t s = (hipStream_t)stream;
     if (!stream_ok(s, c->device)) return LMPC_ERR_ARG;
     double* w = d_slack ? d_slack : c->d_out;  // no inequality rows: the kernel writes no slack
-    return launch(c, d_tasks, batch, d_x, w, d_status, d_iters, s) == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
+    return launch(c, d_tasks, batch, d_x, w, d_status, d_iters, d_z, d_zcols, s) == hipSuccess ? LMPC_OK
+                                                                                                  : LMPC_ERR_LAUNCH;
+}
+
+int lmpc_hoqp_solve_device(lmpc_hoqp_ctx* c, const double* d_tasks, int batch, double* d_x, double* d_slack,
+                           int32_t* d_status, int32_t* d_iters, void* stream) {
+    return lmpc_hoqp_solve_device_z(c, d_tasks, batch, d_x, d_slack, d_status, d_iters, nullptr, nullptr, stream);
 }
 
 int lmpc_hoqp_sync(lmpc_hoqp_ctx* c) {

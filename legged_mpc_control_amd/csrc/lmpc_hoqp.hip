@@ -941,6 +941,7 @@ template <int NP>
 __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const double* __restrict__ recs,
                                                        double* __restrict__ xout, double* __restrict__ wout,
                                                        int32_t* __restrict__ status, int32_t* __restrict__ iters,
+                                                       double* __restrict__ zout, int32_t* __restrict__ zcols,
                                                        double* __restrict__ scratch, int batch) {
     extern __shared__ __attribute__((aligned(16))) double hq_smem[];
     const int b = blockIdx.x;
@@ -1277,6 +1278,17 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             zident = false;
             nd = nd_next;
         }
+        if (zout) {
+            // getStackedZMatrix() of this level (HoQp.h:26-29): the basis the levels below work in, n x nd, in an
+            // n x n block whose columns nd.. are zero (rows written coalesced, lane = column)
+            gdouble* zo = (gdouble*)(zout + ((int64_t)b * P.L + l) * P.n * P.n);
+            const gdouble* Zl = zident ? nullptr : zbuf[zc];
+            for (int r = 0; r < P.n; ++r)
+                if (lane < P.n)
+                    zo[(int64_t)r * P.n + lane] =
+                        lane < nd ? (Zl ? (double)Zl[(int64_t)r * P.np + lane] : (r == lane ? 1.0 : 0.0)) : 0.0;
+            if (zcols && lane == 0) zcols[(int64_t)b * P.L + l] = nd;
+        }
         p = nr;
         HSTAMP(7);
         if (nonfin) {
@@ -1297,6 +1309,10 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         for (int l = 0; l < P.L; ++l)
             if (lane < P.n) xout[((int64_t)b * P.L + l) * P.n + lane] = 0.0;
         for (int r = lane; r < P.slack_len; r += 64) wout[(int64_t)b * P.slack_len + r] = 0.0;
+        if (zout) {
+            for (int64_t e = lane; e < (int64_t)P.L * P.n * P.n; e += 64) zout[(int64_t)b * P.L * P.n * P.n + e] = 0.0;
+            if (zcols && lane < P.L) zcols[(int64_t)b * P.L + lane] = 0;
+        }
         st = 2;
     }
     if (status && lane == 0) status[b] = st;
@@ -1316,25 +1332,25 @@ extern "C" int lmpc_debug_hoqp_substamps(unsigned long long* out, int n) {
 #endif
 
 hipError_t launch_hoqp(const HoqpDev& P, const double* rec, int batch, double* x, double* w, int32_t* status,
-                       int32_t* iters, double* scratch, hipStream_t stream) {
+                       int32_t* iters, double* zout, int32_t* zcols, double* scratch, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     const size_t lds = hq_lds_doubles(P) * sizeof(double);
     switch (P.np) {
         case 16:
             hipLaunchKernelGGL(lmpc_hoqp_kernel<16>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
-                               scratch, batch);
+                               zout, zcols, scratch, batch);
             break;
         case 32:
             hipLaunchKernelGGL(lmpc_hoqp_kernel<32>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
-                               scratch, batch);
+                               zout, zcols, scratch, batch);
             break;
         case 48:
             hipLaunchKernelGGL(lmpc_hoqp_kernel<48>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
-                               scratch, batch);
+                               zout, zcols, scratch, batch);
             break;
         case 64:
             hipLaunchKernelGGL(lmpc_hoqp_kernel<64>, dim3(batch), dim3(64), lds, stream, P, rec, x, w, status, iters,
-                               scratch, batch);
+                               zout, zcols, scratch, batch);
             break;
         default:
             return hipErrorInvalidValue;

@@ -4,7 +4,7 @@ Host-side mirror of the reference's interface over the C-ABI of include/lmpc/lmp
 
   * `Task` -- include/wbc_ctrl/task.h:16-64 (a x = b, d x <= f; `+` stacks self first);
   * `HoQp(task, higher_problem=None)` -- include/wbc_ctrl/HoQp.h:17-50: each object is one priority level,
-    solved on construction (HoQp.cpp:19-27); getSolutions(), getStackedSlackSolutions(),
+    solved on construction (HoQp.cpp:19-27); getSolutions(), getStackedSlackSolutions(), getStackedZMatrix(),
     getSlackedNumVars(), getStackedTasks() as in the reference.  The chain is solved on the device in one
     launch (every level's tasks are passed down; the higher levels' results are recomputed identically);
   * `HoqpBatch` -- the batched form: many robots, one launch, host or device (torch) buffers.
@@ -140,9 +140,10 @@ class HoqpBatch:
         with self._lock:
             N.check(self._L.lmpc_hoqp_set_options(self._ctx, ctypes.byref(o)), "lmpc_hoqp_set_options")
 
-    def solve(self, records: np.ndarray):
+    def solve(self, records: np.ndarray, with_z: bool = False):
         """Host path.  records [B][rec_len] -> x [B][levels][n], slack [B][total ineq rows], status [B],
-        iters [B][levels]."""
+        iters [B][levels]; with_z: also z [B][levels][n][n] and zcols [B][levels], every level's
+        getStackedZMatrix() in the first zcols columns (lmpc_hoqp_solve_batch_z)."""
         rec = np.ascontiguousarray(records, dtype=np.float64).reshape(-1, self.rec_len)
         B = rec.shape[0]
         x = np.zeros((B, self.levels, self.n))
@@ -150,14 +151,22 @@ class HoqpBatch:
         st = np.zeros(B, dtype=np.int32)
         it = np.zeros((B, self.levels), dtype=np.int32)
         dp, i32p = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
+        z = np.zeros((B, self.levels, self.n, self.n)) if with_z else None
+        zc = np.zeros((B, self.levels), dtype=np.int32) if with_z else None
         with self._lock:
-            N.check(self._L.lmpc_hoqp_solve_batch(self._ctx, rec.ctypes.data_as(dp), B, x.ctypes.data_as(dp),
-                                                  w.ctypes.data_as(dp), st.ctypes.data_as(i32p),
-                                                  it.ctypes.data_as(i32p)), "lmpc_hoqp_solve_batch")
+            N.check(self._L.lmpc_hoqp_solve_batch_z(self._ctx, rec.ctypes.data_as(dp), B, x.ctypes.data_as(dp),
+                                                    w.ctypes.data_as(dp), st.ctypes.data_as(i32p),
+                                                    it.ctypes.data_as(i32p),
+                                                    z.ctypes.data_as(dp) if with_z else None,
+                                                    zc.ctypes.data_as(i32p) if with_z else None),
+                    "lmpc_hoqp_solve_batch_z")
+        if with_z:
+            return x, w[:, :self.slack_len], st, it, z, zc
         return x, w[:, :self.slack_len], st, it
 
-    def solve_device(self, d_rec, d_x, d_w, d_status=None, d_iters=None, stream=None):
-        """Device path on torch tensors (resident in HBM), asynchronous on `stream` (default: torch's current)."""
+    def solve_device(self, d_rec, d_x, d_w, d_status=None, d_iters=None, stream=None, d_z=None, d_zcols=None):
+        """Device path on torch tensors (resident in HBM), asynchronous on `stream` (default: torch's current);
+        d_z [B][levels][n][n] / d_zcols [B][levels]: every level's getStackedZMatrix() (optional)."""
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -170,11 +179,18 @@ class HoqpBatch:
             check_device_tensor("d_status", d_status, torch.int32, (B,), dev)
         if d_iters is not None:
             check_device_tensor("d_iters", d_iters, torch.int32, (B, self.levels), dev)
+        if d_z is not None:
+            check_device_tensor("d_z", d_z, torch.float64, (B, self.levels, self.n, self.n), dev)
+        if d_zcols is not None:
+            if d_z is None:
+                raise ValueError("d_zcols needs d_z")
+            check_device_tensor("d_zcols", d_zcols, torch.int32, (B, self.levels), dev)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         with self._lock:
-            N.check(self._L.lmpc_hoqp_solve_device(self._ctx, ptr(d_rec), B, ptr(d_x), ptr(d_w), ptr(d_status),
-                                                   ptr(d_iters), ctypes.c_void_p(s.cuda_stream)),
-                    "lmpc_hoqp_solve_device")
+            N.check(self._L.lmpc_hoqp_solve_device_z(self._ctx, ptr(d_rec), B, ptr(d_x), ptr(d_w), ptr(d_status),
+                                                     ptr(d_iters), ptr(d_z), ptr(d_zcols),
+                                                     ctypes.c_void_p(s.cuda_stream)),
+                    "lmpc_hoqp_solve_device_z")
 
 
 def check_device_tensor(name, t, dtype, shape, device, allow_shape=None):
@@ -218,8 +234,9 @@ class HoQp:
         self._level = len(chain) - 1
         dims = dims_of(chain)
         batch = _batch_for(dims, device)
-        x, w, st, it = batch.solve(pack(chain, dims)[None, :])
+        x, w, st, it, z, zc = batch.solve(pack(chain, dims)[None, :], with_z=True)
         self._x = x[0, self._level].copy()
+        self._z = z[0, self._level, :, :int(zc[0, self._level])].copy()
         self._slack = w[0, :sum(dims.ineq_rows[:self._level + 1])].copy()
         self.status = int(st[0])
         self.iterations = it[0].copy()
@@ -240,6 +257,5 @@ class HoQp:
     def getSlackedNumVars(self) -> int:  # HoQp.h:47-50
         return self._stacked.d.shape[0]
 
-    def getStackedZMatrix(self):  # HoQp.h:26-29
-        raise NotImplementedError("the null-space basis stays on the device (lmpc_hoqp.hip); only the chain's "
-                                  "solutions and slacks are returned")
+    def getStackedZMatrix(self) -> np.ndarray:  # HoQp.h:26-29: Z after this level (n x nd), Eigen's FullPivLU basis
+        return self._z.copy()

@@ -69,6 +69,21 @@ int main() {
     for (long i = 0; i < y.size(); ++i) fails += !(y[i] <= task_1.f_[i] + slack_1[i]);
     fails += ho_qp_0->status() != 0 || ho_qp_1->status() != 0;
     fails += ho_qp_1->getSlackedNumVars() != 4 || slack_1.size() != 4;
+    // getStackedZMatrix() (HoQp.h:26-29, not checked by the reference test): 4 - rank 2 = 2 columns after level 0,
+    // spanning ker(a_0): a_0 Z_0 = 0; after level 1 (task_1.a_ = ones, one more independent row) 1 column with
+    // a_0 Z_1 = a_1 Z_1 = 0
+    const matrix_t z0 = ho_qp_0->getStackedZMatrix(), z1 = ho_qp_1->getStackedZMatrix();
+    fails += z0.rows() != 4 || z0.cols() != 2 || z1.rows() != 4 || z1.cols() != 1;
+    auto null_of = [&](const matrix_t& a, const matrix_t& z) {
+        for (long i = 0; i < a.rows(); ++i)
+            for (long j = 0; j < z.cols(); ++j) {
+                double t = 0.0;
+                for (long k = 0; k < a.cols(); ++k) t += a(i, k) * z(k, j);
+                if (std::fabs(t) > 1e-12) return false;
+            }
+        return true;
+    };
+    fails += !null_of(task_0.a_, z0) || !null_of(task_0.a_, z1) || !null_of(task_1.a_, z1);
     std::printf("ho_qp_test %s\n", fails ? "FAILED" : "OK");
     return fails ? 1 : 0;
 }

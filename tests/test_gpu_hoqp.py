@@ -226,6 +226,50 @@ def test_wbc_tasks_on_device_then_solve(hq):
     assert np.all(st_h <= 1) and np.mean(st_h == 0) >= 0.98 and np.array_equal(d_st.cpu().numpy(), st_h)
 
 
+@pytest.mark.parametrize("group", ["wbc", "rand3", "n20", "n64", "exhaust", "ref"])
+def test_stacked_z_matrix(hq, group):
+    """getStackedZMatrix() (HoQp.h:26-29) of every level, from lmpc_hoqp_solve_batch_z: Eigen's FullPivLU kernel
+    basis chained as HoQp.cpp:147-156 does, against the restatement's (oracle/hoqp.py fullpivlu_kernel, the same
+    pivoting and basis), column counts included; columns past the count are zero.  The device path returns the
+    same bits as the host path, and the HoQp mirror's getter the chain's last level."""
+    import torch
+
+    from oracle import hoqp as Q
+
+    g = load(group)
+    dims = dims_from(g["dims"])
+    B = g["rec"].shape[0]
+    solver = hq.HoqpBatch(dims, B)
+    x, w, st, it, z, zc = solver.solve(g["rec"], with_z=True)
+    n = dims.num_vars
+    worst = 0.0
+    for b in range(B):
+        Z = np.eye(n)
+        for l, (a, bb, d, f) in enumerate(unpack(g["rec"][b], dims)):
+            if a.shape[0]:
+                Z = Z @ Q.fullpivlu_kernel(a @ Z)
+            k = int(zc[b, l])
+            assert k == Z.shape[1], f"chain {b} level {l}: {k} columns, the restatement has {Z.shape[1]}"
+            assert np.all(z[b, l, :, k:] == 0.0)
+            worst = max(worst, float(np.max(np.abs(z[b, l, :, :k] - Z))) / (1.0 + float(np.max(np.abs(Z)))))
+    assert worst <= 1e-10, f"{group}: stacked Z differs by {worst:.2e}"
+    dev = torch.device("cuda:0")
+    d_rec = torch.from_numpy(g["rec"]).to(dev)
+    d_x = torch.empty((B, dims.num_levels, n), dtype=torch.float64, device=dev)
+    d_w = torch.empty((B, max(solver.slack_len, 1)), dtype=torch.float64, device=dev)
+    d_z = torch.full((B, dims.num_levels, n, n), 7.0, dtype=torch.float64, device=dev)
+    d_zc = torch.empty((B, dims.num_levels), dtype=torch.int32, device=dev)
+    solver.solve_device(d_rec, d_x, d_w, d_z=d_z, d_zcols=d_zc)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_z.cpu().numpy(), z) and np.array_equal(d_zc.cpu().numpy(), zc)
+    if group == "ref":
+        t0, t1 = [hq.Task(a, bb, d, f) for (a, bb, d, f) in unpack(g["rec"][0], dims)]
+        h0 = hq.HoQp(t0)
+        h1 = hq.HoQp(t1, h0)
+        assert np.array_equal(h0.getStackedZMatrix(), z[0, 0, :, :zc[0, 0]])
+        assert np.array_equal(h1.getStackedZMatrix(), z[0, 1, :, :zc[0, 1]])
+
+
 def test_reference_ho_qp_test_program():
     """The reference's ho_qp_test.cpp checks, in C++, against legged::HoQp on the GPU (tests/cpp/ho_qp_test.cpp)."""
     import subprocess
