@@ -230,7 +230,19 @@ __device__ __forceinline__ double n_eval(const NCoef& n, double ck, double sk, d
 // W: the calling kernel's waves-per-SIMD budget -- one copy per budget, so each copy is register-
 // allocated for its caller's occupancy (a shared callee would take the larger budget into both)
 template <int W>
-__device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, int H, const double dt,
+// Diagnostic builds only (tools/build, -DLMPC_FACTOR_INLINE / -DLMPC_SOLVE_INLINE): the factor / solve inlined at
+// their one call site instead of outlined (A/B of the call-saved register traffic).
+#ifdef LMPC_FACTOR_INLINE
+#define LMPC_FACTOR_ATTR always_inline
+#else
+#define LMPC_FACTOR_ATTR noinline
+#endif
+#ifdef LMPC_SOLVE_INLINE
+#define LMPC_SOLVE_ATTR always_inline
+#else
+#define LMPC_SOLVE_ATTR noinline
+#endif
+__device__ __attribute__((LMPC_FACTOR_ATTR)) void riccati_factor(const Smem S, gdouble* __restrict__ gs, int H, const double dt,
                                                          const int lane) {
     H = __builtin_amdgcn_readfirstlane(H);  // wave-uniform (arguments arrive in VGPRs): scalar loop control
     const int lc = lane & 15, lr = lane >> 4;  // accumulator layout: column lc, rows lr + 4i
@@ -491,7 +503,7 @@ __device__ __attribute__((noinline)) void riccati_factor(const Smem S, gdouble* 
 // forward sweep (their L2 latency hides behind the serial recursion).
 // ---------------------------------------------------------------------------
 template <int NT12, int W>
-__device__ __attribute__((noinline)) void riccati_solve(const Smem S, const gdouble* __restrict__ gs, int H,
+__device__ __attribute__((LMPC_SOLVE_ATTR)) void riccati_solve(const Smem S, const gdouble* __restrict__ gs, int H,
                                                         const double dt, const int lane) {
     constexpr int NT6 = (NT12 + 1) / 2;
     H = __builtin_amdgcn_readfirstlane(H);  // wave-uniform (arguments arrive in VGPRs): scalar loop control

@@ -20,6 +20,9 @@ from legged_mpc_control_amd import synth  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
+CORR = [0, 0]  # gondzio: correctors accepted / rejected
+
+
 def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
     nls = len(st)
     mu_f, fmax = p.mu, p.f_max
@@ -63,7 +66,27 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
         ds = -(C @ u - bvec) - s
         dz = (smu - z * s - dsa * dza - z * ds) / s
         df = u - f
-        if rule == "split":
+        if rule.startswith("gondzio"):  # multiple centrality correctors (Colombo & Gondzio), same factorisation
+            kmax = int(rule[7:] or 2)
+            a0 = min(step(s, ds), step(z, dz))
+            for _ in range(kmax):
+                at = min(1.0, 1.5 * a0 + 0.1)
+                v = (s + at * ds) * (z + at * dz)
+                mt = smu if smu > 0 else mu * 0.1
+                t = np.where(v < 0.1 * mt, 0.1 * mt - v, np.where(v > 10 * mt, np.maximum(10 * mt - v, -10 * mt), 0.0))
+                dfc = Kinv @ -(C.T @ (t / s))
+                dsc = -C @ dfc
+                dzc = (t - z * dsc) / s
+                ds2, dz2, df2 = ds + dsc, dz + dzc, df + dfc
+                a1 = min(step(s, ds2), step(z, dz2))
+                if a1 >= a0 + 0.1 * (at - a0) * 0.1 + 1e-12 and a1 > a0:
+                    ds, dz, df, a0 = ds2, dz2, df2, a1
+                    CORR[0] += 1
+                else:
+                    CORR[1] += 1
+                    break
+            ap = ad = min(1.0, 0.99 * a0)
+        elif rule == "split":
             ap = min(1.0, 0.99 * step(s, ds))
             ad = min(1.0, 0.99 * step(z, dz))
         else:
@@ -73,6 +96,18 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
         s = s + ap * ds
         z = z + ad * dz
         it += 1
+
+
+def ipm_history(Hm, g, st, p, tol=1e-8, max_iter=40):
+    """Run the kernel's rule ('same') and keep every iterate (f, s, z, mu) for hand-over studies."""
+    hist = []
+    nls = len(st)
+    for k in range(1, max_iter + 1):
+        f, s, z, it = ipm(Hm, g, st, p, "same", tol=tol, max_iter=k)
+        hist.append((f, s, z, float(s @ z / len(s))))
+        if it < k:
+            break
+    return hist
 
 
 def active_guess(f, s, z, fmax):
@@ -89,7 +124,38 @@ def active_guess(f, s, z, fmax):
     return act
 
 
+def handover(cnt=256, mthr=1e-3, stable=1):
+    """Hand the IPM iterate to the polish once the active-set guess has been stable for `stable` iterations and the
+    mean complementarity is below mthr; a failed polish falls back to the full IPM + polish (its rounds paid)."""
+    p, H, rec, con = synth.config_batch(2, count=cnt)
+    op = O.params_from(p)
+    base, new = [], []
+    for b in range(cnt):
+        Hm, g, st, idx = reduced_qp(op, H, rec[b], con[b])
+        hist = ipm_history(Hm, g, st, p)
+        f, s, z, mu = hist[-1]
+        _, rd, ok = polish(Hm, g, active_guess(f, s, z, p.f_max), p.mu, p.f_max)
+        full = 55e3 + 42e3 * len(hist) + 45e3 * rd
+        base.append(full)
+        cyc = None
+        for k in range(stable, len(hist)):
+            gk = active_guess(*hist[k][:3], p.f_max)
+            if hist[k][3] < mthr and all(active_guess(*hist[k - j][:3], p.f_max) == gk for j in range(1, stable + 1)):
+                _, rdk, okk = polish(Hm, g, gk, p.mu, p.f_max)
+                cyc = 55e3 + 42e3 * (k + 1) + 45e3 * rdk if okk else full + 45e3 * rdk
+                break
+        new.append(cyc if cyc is not None else full)
+    base, new = np.array(base), np.array(new)
+    print(f"handover mthr {mthr:g} stable {stable}: mean {base.mean() / 1e3:.0f}k -> {new.mean() / 1e3:.0f}k, "
+          f"max {base.max() / 1e3:.0f}k -> {new.max() / 1e3:.0f}k, p99 {np.percentile(new, 99) / 1e3:.0f}k", flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "handover":
+        for mthr in (1e-2, 1e-3, 1e-4):
+            for stable in (1, 2):
+                handover(int(sys.argv[2]) if len(sys.argv) > 2 else 256, mthr, stable)
+        return
     cnt = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     rules = sys.argv[2].split(",") if len(sys.argv) > 2 else ["same", "split", "adapt"]
     p, H, rec, con = synth.config_batch(2, count=cnt)
@@ -104,6 +170,9 @@ def main():
             its.append(it)
             rds.append(rd)
             cyc.append(55e3 + 42e3 * it + 45e3 * rd)
+        if rule.startswith("gondzio"):
+            print(f"  correctors accepted {CORR[0]} rejected {CORR[1]} (each ~3 k cycles: one more solve)")
+            CORR[0] = CORR[1] = 0
         its, rds, cyc = np.array(its), np.array(rds), np.array(cyc)
         print(f"{rule:6s}: ipm mean {its.mean():.2f} max {its.max()} | rounds mean {rds.mean():.2f} max {rds.max()} | "
               f"model cycles mean {cyc.mean() / 1e3:.0f} k max {cyc.max() / 1e3:.0f} k p99 {np.percentile(cyc, 99) / 1e3:.0f} k"
