@@ -279,7 +279,10 @@ def main():
     # and the fp64 flops the kernels really executed (SQ_INSTS_VALU_FLOPS_FP64 + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64)
     traffic_bytes = None
     executed = None
-    wl = (wl_name if mode == ("gi" if args.config == 4 else "ipm") else f"{wl_name}/{mode}") if args.batch is None else None
+    # the committed PMC figures are keyed by workload, plus "/<mode>" when --dense overrides the config's own path
+    # (configs 3 and 5 run the Riccati kernel by default: H > 16 has no dense path)
+    overridden = args.dense is not None and args.dense != ("gi" if args.config == 4 else "ipm")
+    wl = (f"{wl_name}/{mode}" if overridden else wl_name) if args.batch is None else None
     try:
         tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
         if wl in tr:
