@@ -7,9 +7,9 @@ OUT=gpurun_out/prof_hoqp
 rm -rf $OUT
 mkdir -p $OUT
 rp() { timeout -k 10 300 rocprofv3 "$@"; }
-rp --kernel-trace --stats -d $OUT/hq -o hq --output-format csv -- python3 tools/bench_hoqp.py --steps 20 --warmup 3 --no-cpu > $OUT/hq_bench.log 2>&1 &&
-rp --pmc FETCH_SIZE --kernel-trace -d $OUT/fhq -o fhq --output-format csv -- python3 tools/bench_hoqp.py --steps 3 --warmup 1 --no-cpu > $OUT/fhq.log 2>&1 &&
-rp --pmc WRITE_SIZE --kernel-trace -d $OUT/whq -o whq --output-format csv -- python3 tools/bench_hoqp.py --steps 3 --warmup 1 --no-cpu > $OUT/whq.log 2>&1
+rp --kernel-trace --stats -d $OUT/hq -o hq --output-format csv -- python3 tools/bench_hoqp.py --steps 20 --warmup 3 --no-cpu $HOQP_ARGS > $OUT/hq_bench.log 2>&1 &&
+rp --pmc FETCH_SIZE --kernel-trace -d $OUT/fhq -o fhq --output-format csv -- python3 tools/bench_hoqp.py --steps 3 --warmup 1 --no-cpu $HOQP_ARGS > $OUT/fhq.log 2>&1 &&
+rp --pmc WRITE_SIZE --kernel-trace -d $OUT/whq -o whq --output-format csv -- python3 tools/bench_hoqp.py --steps 3 --warmup 1 --no-cpu $HOQP_ARGS > $OUT/whq.log 2>&1
 rc=$?
 echo "profile_hoqp rc=$rc"
 find $OUT -name "*.csv" | head -20
