@@ -79,6 +79,8 @@ def test_create_and_solve_reject_bad_arguments_without_gpu():
     assert lib.lmpc_hoqp_create(None, 4, 0, ctypes.byref(ctx)) == -1
     assert lib.lmpc_hoqp_solve_batch(None, None, 1, None, None, None, None) == -1
     assert lib.lmpc_hoqp_solve_device(None, None, 1, None, None, None, None, None) == -1
+    assert lib.lmpc_hoqp_solve_batch_z(None, None, 1, None, None, None, None, None, None) == -1
+    assert lib.lmpc_hoqp_solve_device_z(None, None, 1, None, None, None, None, None, None, None) == -1
     assert lib.lmpc_hoqp_sync(None) == -1
     if torch.cuda.device_count() == 0:
         assert lib.lmpc_hoqp_create(ctypes.byref(d), 4, 0, ctypes.byref(ctx)) == -2
