@@ -393,9 +393,17 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
 struct DiagInv {
     d4 ui, uit;
 };
-// Outlined (one call site): the elimination gets the caller-saved registers to itself instead of
-// competing with the factor tiles and the leg state that are live around it.
-static __device__ __attribute__((noinline)) DiagInv diag_inverse(ldouble* scr, d4 M, int amask, int lane) {
+// Inlined at its call sites (round 3): outlined, the call cost the caller ~1.7 k cycles per tile in argument /
+// result moves and in the caller-saved registers it had to park around the call (5.6 k cycles per tile in the
+// kernel vs 3.9 k alone, tools/ubench/diag_parts.hip); inlined, config 2 runs 2 % faster (0.2304 -> 0.2259 ms,
+// tools/ab_bench.sh, two alternating runs each; bit-identical results).  -DLMPC_DIAG_OUTLINE (diagnostic builds
+// only) restores the call.
+#ifdef LMPC_DIAG_OUTLINE
+#define LMPC_DIAG_ATTR noinline
+#else
+#define LMPC_DIAG_ATTR always_inline
+#endif
+static __device__ __attribute__((LMPC_DIAG_ATTR)) DiagInv diag_inverse(ldouble* scr, d4 M, int amask, int lane) {
     amask = __builtin_amdgcn_readfirstlane(amask);  // uniform (tile_mask), but arguments arrive in VGPRs
     // staging of the registers that hold the pivot rows (i0, i1): every lane stores its value unconditionally, so
     // row r of register i sits at 16 (r & 3) + c (+64 for i1) -- static read offsets, no per-lane address select

@@ -1,0 +1,269 @@
+// Dev microbenchmark: where a pivot of the dense path's diagonal-tile inverse (lmpc::diag_inverse) spends its
+// cycles.  Variants of the same loop on one wave (a fixed SPD tile, 64 calls back to back):
+//   0  the product code (a copy of diag_inverse);
+//   1  without the W = L^-1 chain (T's pivot chain and rank-3 updates only);
+//   2  as 1, pivot rows by readlane / bpermute instead of the LDS write -> read round trip;
+//   3  as 1, without T's rank-3 MFMA (the next pivot does not wait for the matrix core).
+// Build from the repo root:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I legged_mpc_control_amd/csrc \
+//         -o tools/ubench/diag_parts tools/ubench/diag_parts.hip
+#include "../../legged_mpc_control_amd/csrc/lmpc_dense.hip"
+
+#include <cstdio>
+
+namespace lmpc {
+template <int V>
+static __device__ __attribute__((noinline)) DiagInv diag_v(ldouble* scr, d4 M, int amask, int lane) {
+    amask = __builtin_amdgcn_readfirstlane(amask);
+    ldouble* sT = scr;
+    ldouble* sW = scr + 128;
+    ldouble* tr = scr + 256;
+    const int c = lane & 15, g = lane >> 4;
+    d4 T = M, W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) W[i] = (4 * i + g == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int blk = 0; blk < 5; ++blk) {
+        if (!((amask >> blk) & 1)) continue;
+        const int o = 3 * blk;
+        const int i0 = o >> 2, i1 = (o + 2) >> 2;
+        const int ra = 4 * i0 + g - o, rb = 4 * i1 + g - o;
+        const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
+        auto so = [&](int a) { return ((o + a) >> 2 == i0 ? 0 : 64) + 16 * ((o + a) & 3); };
+        double p00, p10, p11, p20, p21, p22, t0, t1, t2;
+        if (V == 2) {
+            // element (r, col) of T: register r >> 2 of lane 16 (r & 3) + col
+            auto el = [&](int r, int col) {
+                const double v = T[r >> 2];
+                const int src = 16 * (r & 3) + col;
+                const int lo = __builtin_amdgcn_readlane(__builtin_bit_cast(int2, v).x, src);
+                const int hi = __builtin_amdgcn_readlane(__builtin_bit_cast(int2, v).y, src);
+                return __builtin_bit_cast(double, int2{lo, hi});
+            };
+            p00 = el(o, o); p10 = el(o + 1, o); p11 = el(o + 1, o + 1);
+            p20 = el(o + 2, o); p21 = el(o + 2, o + 1); p22 = el(o + 2, o + 2);
+            auto col = [&](int r) {
+                const double v = T[r >> 2];
+                const int src = (16 * (r & 3) + c) * 4;
+                const int lo = __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int2, v).x);
+                const int hi = __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int2, v).y);
+                return __builtin_bit_cast(double, int2{lo, hi});
+            };
+            t0 = col(o); t1 = col(o + 1); t2 = col(o + 2);
+        } else {
+            LMPC_SYNC();
+            sT[lane] = T[i0];
+            if (i1 != i0) sT[64 + lane] = T[i1];
+            LMPC_SYNC();
+            p00 = sT[so(0) + o]; p10 = sT[so(1) + o]; p11 = sT[so(1) + o + 1];
+            p20 = sT[so(2) + o]; p21 = sT[so(2) + o + 1]; p22 = sT[so(2) + o + 2];
+            t0 = sT[so(0) + c]; t1 = sT[so(1) + c]; t2 = sT[so(2) + c];
+        }
+        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+        if (V == 0) {
+            sW[lane] = W[i0];
+            if (i1 != i0) sW[64 + lane] = W[i1];
+            W[i0] = ina ? 0.0 : W[i0];
+            if (i1 != i0) W[i1] = inb ? 0.0 : W[i1];
+            LMPC_SYNC();
+            w0 = sW[so(0) + c]; w1 = sW[so(1) + c]; w2 = sW[so(2) + c];
+        }
+        const double m11 = fma(p00, p11, -p10 * p10);
+        const double c00 = fma(p11, p22, -p21 * p21), c01 = fma(p10, p22, -p21 * p20), c02 = fma(p10, p21, -p11 * p20);
+        const double det = fma(p00, c00, fma(-p10, c01, p20 * c02));
+        const double i00 = rsq_nr(p00), r1 = rsq_nr(m11), r2 = rsq_nr(det);
+        const double l10 = p10 * i00, l20 = p20 * i00;
+        const double i11 = (p00 * i00) * r1;
+        const double l21 = fma(-l20, l10, p21) * i11;
+        const double i22 = (m11 * r1) * r2;
+        const double x0 = t0 * i00;
+        const double x1 = fma(-l10, x0, t1) * i11;
+        const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
+        const double xs = g == 0 ? x0 : g == 1 ? x1 : x2;
+        const double av = (c > o + 2 && g < 3) ? xs : 0.0;
+        if (V == 0) {
+            const double v0 = w0 * i00;
+            const double v1 = fma(-l10, v0, w1) * i11;
+            const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
+            const double vs = g == 0 ? v0 : g == 1 ? v1 : v2;
+            const double bv = g < 3 ? vs : 0.0;
+            const bool cp = c >= o && c <= o + 2;
+            const double aw = cp ? (g == c - o ? 1.0 : 0.0) : -av;
+            W = MFMA64(aw, bv, W);
+        } else {
+            W[0] += av;  // keep the chain's result live
+        }
+        if (V == 3) T[blk & 3] += 1e-300 * av;
+        else T = MFMA64(-av, av, T);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tr[c * 17 + 4 * i + g] = W[i];
+    LMPC_SYNC();
+    DiagInv out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        out.uit[i] = W[i];
+        out.ui[i] = tr[(4 * i + g) * 17 + c];
+    }
+    return out;
+}
+
+// variant 4: the W = L^-1 update of pivot k-1 is issued in pivot k's iteration, interleaved with pivot k's T
+// chain (no data dependency between them), and the last one after the loop
+static __device__ __attribute__((noinline)) DiagInv diag_v4(ldouble* scr, d4 M, int amask, int lane) {
+    amask = __builtin_amdgcn_readfirstlane(amask);
+    ldouble* sT = scr;
+    ldouble* sW = scr + 128;
+    ldouble* tr = scr + 256;
+    const int c = lane & 15, g = lane >> 4;
+    d4 T = M, W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) W[i] = (4 * i + g == c) ? 1.0 : 0.0;
+    // pending W update (pivot k-1): block offset, its pivot scalars and this lane's av
+    int po = -1;
+    double q00 = 0, q10 = 0, q20 = 0, q11 = 0, q21 = 0, q22 = 0, pav = 0;
+    auto wupdate = [&](int o, double i00, double l10, double l20, double i11, double l21, double i22, double av) {
+        const int i0 = o >> 2, i1 = (o + 2) >> 2;
+        const int ra = 4 * i0 + g - o, rb = 4 * i1 + g - o;
+        const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
+        auto so = [&](int a) { return ((o + a) >> 2 == i0 ? 0 : 64) + 16 * ((o + a) & 3); };
+        sW[lane] = W[i0];
+        if (i1 != i0) sW[64 + lane] = W[i1];
+        W[i0] = ina ? 0.0 : W[i0];
+        if (i1 != i0) W[i1] = inb ? 0.0 : W[i1];
+        LMPC_SYNC();
+        const double w0 = sW[so(0) + c], w1 = sW[so(1) + c], w2 = sW[so(2) + c];
+        const double v0 = w0 * i00;
+        const double v1 = fma(-l10, v0, w1) * i11;
+        const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
+        const double vs = g == 0 ? v0 : g == 1 ? v1 : v2;
+        const double bv = g < 3 ? vs : 0.0;
+        const bool cp = c >= o && c <= o + 2;
+        const double aw = cp ? (g == c - o ? 1.0 : 0.0) : -av;
+        W = MFMA64(aw, bv, W);
+    };
+#pragma unroll
+    for (int blk = 0; blk < 5; ++blk) {
+        if (!((amask >> blk) & 1)) continue;
+        const int o = 3 * blk;
+        const int i0 = o >> 2, i1 = (o + 2) >> 2;
+        auto so = [&](int a) { return ((o + a) >> 2 == i0 ? 0 : 64) + 16 * ((o + a) & 3); };
+        LMPC_SYNC();
+        sT[lane] = T[i0];
+        if (i1 != i0) sT[64 + lane] = T[i1];
+        LMPC_SYNC();
+        const double p00 = sT[so(0) + o], p10 = sT[so(1) + o], p11 = sT[so(1) + o + 1];
+        const double p20 = sT[so(2) + o], p21 = sT[so(2) + o + 1], p22 = sT[so(2) + o + 2];
+        const double t0 = sT[so(0) + c], t1 = sT[so(1) + c], t2 = sT[so(2) + c];
+        if (po >= 0) wupdate(po, q00, q10, q20, q11, q21, q22, pav);
+        const double m11 = fma(p00, p11, -p10 * p10);
+        const double c00 = fma(p11, p22, -p21 * p21), c01 = fma(p10, p22, -p21 * p20), c02 = fma(p10, p21, -p11 * p20);
+        const double det = fma(p00, c00, fma(-p10, c01, p20 * c02));
+        const double i00 = rsq_nr(p00), r1 = rsq_nr(m11), r2 = rsq_nr(det);
+        const double l10 = p10 * i00, l20 = p20 * i00;
+        const double i11 = (p00 * i00) * r1;
+        const double l21 = fma(-l20, l10, p21) * i11;
+        const double i22 = (m11 * r1) * r2;
+        const double x0 = t0 * i00;
+        const double x1 = fma(-l10, x0, t1) * i11;
+        const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
+        const double xs = g == 0 ? x0 : g == 1 ? x1 : x2;
+        const double av = (c > o + 2 && g < 3) ? xs : 0.0;
+        T = MFMA64(-av, av, T);
+        po = o;
+        q00 = i00; q10 = l10; q20 = l20; q11 = i11; q21 = l21; q22 = i22; pav = av;
+    }
+    if (po >= 0) wupdate(po, q00, q10, q20, q11, q21, q22, pav);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tr[c * 17 + 4 * i + g] = W[i];
+    LMPC_SYNC();
+    DiagInv out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        out.uit[i] = W[i];
+        out.ui[i] = tr[(4 * i + g) * 17 + c];
+    }
+    return out;
+}
+}  // namespace lmpc
+
+template <int V>
+__global__ void __launch_bounds__(64) probe(double* out, unsigned long long* cyc, int amask) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int lane = threadIdx.x;
+    const lmpc::DSmem S = lmpc::dcarve(sm, 10);
+    const int lc = lane & 15, lr = lane >> 4;
+    lmpc::d4 M;
+    for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        M[i] = (r == 15 || lc == 15) ? (r == lc ? 1.0 : 0.0) : (r == lc ? 4.0 : 0.0) + 0.1 / (r + lc + 1);
+    }
+    double chk = 0.0;
+    const unsigned long long t0 = __builtin_readcyclecounter();
+    for (int it = 0; it < 64; ++it) {
+        const lmpc::DiagInv di = V == 4 ? lmpc::diag_v4(S.scr, M, amask, lane) : V == 5 ? lmpc::diag_inverse(S.scr, M, amask, lane) : lmpc::diag_v<V>(S.scr, M, amask, lane);
+        chk += di.ui[0] + di.uit[3];
+        M[0] += 1e-300 * chk;
+    }
+    const unsigned long long t1 = __builtin_readcyclecounter();
+    out[lane] = chk;
+    if (lane == 0) cyc[0] = t1 - t0;
+}
+
+__global__ void __launch_bounds__(64) check4(double* out, int amask) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int lane = threadIdx.x;
+    const lmpc::DSmem S = lmpc::dcarve(sm, 10);
+    const int lc = lane & 15, lr = lane >> 4;
+    lmpc::d4 M;
+    for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        // SPD with strong coupling: 0.5 I + (u u' + v v') with u_r = sin(r + 1), v_r = cos(2 r); padding identity
+        const double ur = sin(r + 1.0), uc = sin(lc + 1.0), vr = cos(2.0 * r), vc = cos(2.0 * lc);
+        M[i] = (r == 15 || lc == 15) ? (r == lc ? 1.0 : 0.0) : (r == lc ? 0.5 : 0.0) + ur * uc + vr * vc + 0.01 * (r == lc ? r : 0);
+    }
+    const lmpc::DiagInv a = lmpc::diag_inverse(S.scr, M, amask, lane);
+    const lmpc::DiagInv b = lmpc::diag_v4(S.scr, M, amask, lane);
+    double d = 0.0;
+    for (int i = 0; i < 4; ++i) d = fmax(d, fmax(fabs(a.ui[i] - b.ui[i]), fabs(a.uit[i] - b.uit[i])));
+    out[lane] = d;
+}
+
+template <int V>
+void run(double* out, unsigned long long* cyc, size_t lds) {
+    (void)hipFuncSetAttribute((const void*)probe<V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (int mask : {0x1f, 0x1}) {
+        unsigned long long h = 0;
+        for (int rep = 0; rep < 2; ++rep) {
+            hipLaunchKernelGGL(probe<V>, dim3(1), dim3(64), lds, 0, out, cyc, mask);
+            (void)hipDeviceSynchronize();
+        }
+        (void)hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);
+        printf("variant %d, block mask 0x%02x: %8.0f cycles per call\n", V, mask, (double)h / 64.0);
+    }
+}
+
+int main() {
+    double* out;
+    unsigned long long* cyc;
+    (void)hipMalloc(&out, 64 * sizeof(double));
+    (void)hipMalloc(&cyc, 8);
+    const size_t lds = lmpc::dense_lds_bytes(10);
+    run<0>(out, cyc, lds);
+    run<1>(out, cyc, lds);
+    run<2>(out, cyc, lds);
+    run<3>(out, cyc, lds);
+    run<4>(out, cyc, lds);
+    run<5>(out, cyc, lds);  // the product function itself, for reference
+    // correctness of variant 4 against the product function (max |difference| of Ui, UiT over the tile)
+    (void)hipFuncSetAttribute((const void*)check4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (int mask : {0x1f, 0x15, 0x0e, 0x1}) {
+        double h[64];
+        hipLaunchKernelGGL(check4, dim3(1), dim3(64), lds, 0, out, mask);
+        (void)hipMemcpy(h, out, sizeof(h), hipMemcpyDeviceToHost);
+        double m = 0.0;
+        for (double v : h) m = v > m ? v : m;
+        printf("variant 4 vs diag_inverse, mask 0x%02x: max |diff| %.3e\n", mask, m);
+    }
+    return 0;
+}
