@@ -64,6 +64,38 @@ __device__ unsigned long long lmpc_hoqp_substamps[4096][8];
 #define HSTAMP_FLUSH(b) do {} while (0)
 #endif
 
+// Diagnostic builds only (tools/build, -DHQ_INL_<helper>): that per-iteration helper inlined instead of outlined
+// (A/B of the call overhead against register pressure, tools/hoqp_ab.sh).
+#ifdef HQ_INL_chol_floor
+#define HQ_ATTR_chol_floor always_inline
+#else
+#define HQ_ATTR_chol_floor noinline
+#endif
+#ifdef HQ_INL_chol_solve
+#define HQ_ATTR_chol_solve always_inline
+#else
+#define HQ_ATTR_chol_solve noinline
+#endif
+#ifdef HQ_INL_row_dot
+#define HQ_ATTR_row_dot always_inline
+#else
+#define HQ_ATTR_row_dot noinline
+#endif
+#ifdef HQ_INL_rt_dot
+#define HQ_ATTR_rt_dot always_inline
+#else
+#define HQ_ATTR_rt_dot noinline
+#endif
+#ifdef HQ_INL_hy_dot
+#define HQ_ATTR_hy_dot always_inline
+#else
+#define HQ_ATTR_hy_dot noinline
+#endif
+#ifdef HQ_INL_form_K
+#define HQ_ATTR_form_K always_inline
+#else
+#define HQ_ATTR_form_K noinline
+#endif
 namespace {
 
 struct HS {
@@ -247,7 +279,7 @@ __device__ __forceinline__ void sym_tiles(const ldouble* M, int ld, int rows, co
 // i's multiplier K_ik / d_k is lane-local.  Row updates stop at the last 16-wide block that holds live
 // columns.  The unit lower factor goes back to S.KL (lower part), dI[k] = 1 / d_k.
 template <int NP>
-__device__ __attribute__((noinline)) void chol_floor(const HS& S_, int ls, int nd, int lane) {
+__device__ __attribute__((HQ_ATTR_chol_floor)) void chol_floor(const HS& S_, int ls, int nd, int lane) {
     // local copy: members read through the reference (a flat pointer, which may alias LDS) would be reloaded
     // after every LDS store
     const HS S = S_;
@@ -316,7 +348,7 @@ __device__ __attribute__((noinline)) void chol_floor(const HS& S_, int ls, int n
 // substitution is one readlane broadcast and one fma, in blocks of 8 steps guarded by nd.  A lane's own entry
 // needs no select: its coefficients from its own step on are zero, so its accumulator stops at its solution.
 template <int NP>
-__device__ __attribute__((noinline)) double chol_solve(const HS& S_, int ls, int nd, double rhs, ldouble* out,
+__device__ __attribute__((HQ_ATTR_chol_solve)) double chol_solve(const HS& S_, int ls, int nd, double rhs, ldouble* out,
                                                        int lane) {
     const HS S = S_;
     nd = uni(nd);
@@ -366,7 +398,7 @@ __device__ __attribute__((noinline)) double chol_solve(const HS& S_, int ls, int
 // t = R_r . vec (row r): 16-column blocks up to the level's live tiles, each block's 32 loads issued ahead of
 // its fmas (columns nd..16 nt - 1 of R and of vec are zero)
 template <int NP>
-__device__ __attribute__((noinline)) double row_dot(const HS& S_, int ls, int nd, int r, const ldouble* vec) {
+__device__ __attribute__((HQ_ATTR_row_dot)) double row_dot(const HS& S_, int ls, int nd, int r, const ldouble* vec) {
     const HS S = S_;
     ls = uni(ls);
     const int nt = nd_tiles(uni(nd));
@@ -387,7 +419,7 @@ __device__ __attribute__((noinline)) double row_dot(const HS& S_, int ls, int nd
 }
 // (R' q)_j for lane j: 16-row blocks, each block's 32 loads issued ahead of its fmas; rows past nr are never
 // read (that LDS is not written at this level)
-__device__ __attribute__((noinline)) double rt_dot(const HS& S_, int ls, int nr, const ldouble* q, int lane) {
+__device__ __attribute__((HQ_ATTR_rt_dot)) double rt_dot(const HS& S_, int ls, int nr, const ldouble* q, int lane) {
     const HS S = S_;
     nr = uni(nr);
     ls = uni(ls);
@@ -419,7 +451,7 @@ __device__ __attribute__((noinline)) double rt_dot(const HS& S_, int ls, int nr,
 // every live 16-row block loaded in one batch (one global round trip); rows nd..16 nt - 1 of Hg and y are
 // zero, so the block-wide sum is exact
 template <int NP>
-__device__ __attribute__((noinline)) double hy_dot(const HoqpDev& P_, const gdouble* Hg, const ldouble* y, int nd,
+__device__ __attribute__((HQ_ATTR_hy_dot)) double hy_dot(const HoqpDev& P_, const gdouble* Hg, const ldouble* y, int nd,
                                                    int lane) {
     const HoqpDev P = uniform(P_);
     const int nt = nd_tiles(uni(nd));
@@ -679,7 +711,7 @@ __device__ __attribute__((noinline)) void level_setup(const HoqpDev& P_, const H
 }
 
 // K = Hy + R' diag(wh) R on the matrix cores (lower tiles covering nd) into S.KL.
-__device__ __attribute__((noinline)) void form_K(const HoqpDev& P_, const HS& S_, int nr, int nd, const gdouble* Hg,
+__device__ __attribute__((HQ_ATTR_form_K)) void form_K(const HoqpDev& P_, const HS& S_, int nr, int nd, const gdouble* Hg,
                                                  int lane) {
     const HS S = S_;
     const HoqpDev P = uniform(P_);
