@@ -298,6 +298,8 @@ def main():
                 "achieved": e * B / (kernel_ms * 1e-3) / 1e12,
                 "frac": e * B / (kernel_ms * 1e-3) / 1e12 / roofline.FP64_PEAK_TFLOPS,
                 "valu_share": fl[wl]["valu_flop_per_qp"] / e,
+                # matrix-core utilisation: the executed MFMA flops per second against the fp64 MFMA peak
+                "mfma_frac": fl[wl]["mfma_flop_per_qp"] * B / (kernel_ms * 1e-3) / 1e12 / roofline.FP64_PEAK_TFLOPS,
                 "source": fl[wl]["source"],
             }
     except (OSError, ValueError, KeyError, ZeroDivisionError):
