@@ -57,9 +57,10 @@ typedef struct {
     double tol_mu;      /* stop: mean complementarity <= tol_mu * scale (default 1e-13) */
     double tol_res;     /* stop: max primal / dual residual <= tol_res * scale (default 1e-7) */
     int32_t crossover;  /* round 3: 1 (default) = after each level's interior point, the exact active-set crossover
-                           (taken when it verifies; bits 16-17 of that level's iteration word: 1 tried, 3 taken);
-                           0 = the interior-point iterate as is (about 20 % faster on the WBC, ~1e-9 instead of
-                           ~1e-12 on the WBC, ~1e-4 on degenerate levels) */
+                           (taken when it verifies; bits 16-17 of that level's iteration word: 1 tried, 3 taken):
+                           each level's answer is the active-set optimum qpOASES returns, to rounding;
+                           0 = the interior-point iterate as is (about 13 % faster on the WBC; ~1e-9 instead of
+                           ~1e-12 there, ~1e-4 on degenerate levels) */
 } lmpc_hoqp_options;
 
 typedef struct lmpc_hoqp_ctx lmpc_hoqp_ctx;

@@ -994,6 +994,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     bool nonfin = false;
     // x = 0; Z = I is generated, not stored, until the first level with equalities (zident)
     bool zident = true;
+    bool any_exact = false;  // some level above took its crossover answer (its active rows are exactly tight)
     if (lane < P.np) S.x[lane] = 0.0;
     LMPC_GSYNC();
     int nd = P.n, p = 0, st = 0;
@@ -1066,11 +1067,11 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         const double scale = 1.0 + fmax(wave_max(lane < nd ? fabs(S.c[lane]) : 0.0), wave_max(bmax));
         // A frozen row the crossover of a level above left exactly tight has h = 0 up to rounding (or one ulp
         // below).  Several such rows around a vertex leave the level's feasible set without an interior, and the
-        // interior point then stalls (slacks to the bottom of the range, multipliers unbounded).  With the
-        // crossover on, the interior point sees those bounds raised to HQ_HFLOOR of the scale -- the margin a
-        // level-above iterate would have left -- and the crossover then solves with the true bounds.
+        // interior point then stalls (slacks to the bottom of the range, multipliers unbounded).  Once a level above
+        // took its crossover answer, the interior point sees those bounds raised to HQ_HFLOOR of the scale -- the
+        // margin a level-above iterate would have left -- and the crossover then solves with the true bounds.
         const double hb_true[2] = {W.bd[0], W.bd[1]};
-        if (P.crossover) {
+        if (any_exact) {
 #pragma unroll
             for (int k = 0; k < 2; ++k)
                 if (lane + 64 * k < p) W.bd[k] = fmax(W.bd[k], HQ_HFLOOR * scale);
@@ -1276,6 +1277,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             }
             exact = crossover<NP>(P, S, p, nr, nd, hb_true[0], hb_true[1], fl[0], fl[1], scale, Hg, Tg, lane);
             xo = exact ? 3 : 1;
+            any_exact = any_exact || exact;
         }
         exact = exact || clean;
         // LMPC_QP_CONVERGED: the clean stop, a verified crossover, or -- documented in lmpc_hoqp.h -- the relaxed
