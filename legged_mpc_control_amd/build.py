@@ -15,6 +15,18 @@ ARCH = "gfx950"
 # fp64 MFMA results in AGPRs and moves every element the VALU touches with v_accvgpr_read/write.  Measured:
 # config 2 0.342 -> 0.329 ms, config 4 22.4 -> 22.0 ms (profiles/r02/diag_ab_configs.log).
 HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+# Per-file machine scheduler (round 3, tools/ab_bench.sh / tools/hoqp_ab.sh, alternating runs, bit-identical
+# results): the kernels are lone-wave, issue-in-order chains, and the ILP-oriented strategies interleave their
+# independent work better than the default occupancy-oriented one -- max-ilp: config 2 0.2254-0.2284 ->
+# 0.2198-0.2212 ms, config 4 19.61 -> 19.07-19.18 ms; iterative-ilp: the dual active set (config 2 --dense gi)
+# 0.469 -> 0.459-0.461 ms, the WBC hierarchies 4.89 -> 4.78 ms.  (iterative-ilp crashes the compiler on
+# lmpc_prep.hip, which keeps the default.)
+SCHED_FLAGS = {
+    "lmpc_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "lmpc_dense.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "lmpc_gi.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "lmpc_hoqp.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+}
 
 SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
            "hoqp_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
@@ -44,12 +56,24 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(LIB, deps):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    # one compile per source (per-file scheduler flags), in parallel, then one link
+    procs, objs = [], []
+    for s, src in zip(SOURCES, srcs):
+        obj = os.path.join(objdir, s + ".o")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+               "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj] + HIP_FLAGS + \
+            SCHED_FLAGS.get(s, []) + [src]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd)))
+        objs.append(obj)
+    for cmd, pr in procs:
+        if pr.wait() != 0:
+            raise subprocess.CalledProcessError(pr.returncode, cmd)
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp] + HIP_FLAGS + srcs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
     os.replace(tmp, LIB)
     return LIB
 
@@ -88,15 +112,16 @@ def build_stamps(force: bool = False) -> str:
     return out
 
 
-def build_variant(tag: str, defines, force: bool = False) -> str:
-    """Diagnostic library variant (extra -D flags) under tools/build/; never shipped as the product."""
+def build_variant(tag: str, defines, force: bool = False, flags=()) -> str:
+    """Diagnostic library variant (extra -D flags, extra compiler flags) under tools/build/; never shipped as the
+    product."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     out = os.path.join(ROOT, "tools", "build", f"liblmpc_{tag}.so")
     if not force and not _stale(out, srcs + [os.path.join(CSRC, h) for h in HEADERS]):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + HIP_FLAGS + [f"-D{d}" for d in defines] + srcs
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + HIP_FLAGS + list(flags) + [f"-D{d}" for d in defines] + srcs
     subprocess.run(cmd, check=True)
     return out
 
