@@ -47,6 +47,30 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _compile_lib(out: str, objdir: str, defines=(), flags=(), verbose: bool = False) -> str:
+    """liblmpc from SOURCES: one compile per source (HIP_FLAGS + that file's SCHED_FLAGS + `flags`, -D`defines`),
+    run in parallel, then one link; written to `out` atomically."""
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    procs, objs = [], []
+    for s in SOURCES:
+        obj = os.path.join(objdir, s + ".o")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+               "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj] + HIP_FLAGS + \
+            SCHED_FLAGS.get(s, []) + list(flags) + [f"-D{d}" for d in defines] + [os.path.join(CSRC, s)]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd)))
+        objs.append(obj)
+    for cmd, pr in procs:
+        if pr.wait() != 0:
+            raise subprocess.CalledProcessError(pr.returncode, cmd)
+    tmp = out + ".tmp"
+    subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
+    os.replace(tmp, out)
+    return out
+
+
 def build_native(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [
@@ -55,27 +79,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         os.path.abspath(__file__)]
     if not force and not _stale(LIB, deps):
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    objdir = os.path.join(LIBDIR, "obj")
-    os.makedirs(objdir, exist_ok=True)
-    # one compile per source (per-file scheduler flags), in parallel, then one link
-    procs, objs = [], []
-    for s, src in zip(SOURCES, srcs):
-        obj = os.path.join(objdir, s + ".o")
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
-               "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj] + HIP_FLAGS + \
-            SCHED_FLAGS.get(s, []) + [src]
-        if verbose:
-            print(" ".join(cmd))
-        procs.append((cmd, subprocess.Popen(cmd)))
-        objs.append(obj)
-    for cmd, pr in procs:
-        if pr.wait() != 0:
-            raise subprocess.CalledProcessError(pr.returncode, cmd)
-    tmp = LIB + ".tmp"
-    subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    return _compile_lib(LIB, os.path.join(LIBDIR, "obj"), verbose=verbose)
 
 
 MULTI_LIB = os.path.join(LIBDIR, "liblmpc_multi.so")
@@ -105,11 +109,7 @@ def build_stamps(force: bool = False) -> str:
     out = os.path.join(ROOT, "tools", "build", "liblmpc_stamps.so")
     if not force and not _stale(out, srcs + [os.path.join(CSRC, h) for h in HEADERS]):
         return out
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-DLMPC_STAMPS",
-           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + HIP_FLAGS + srcs
-    subprocess.run(cmd, check=True)
-    return out
+    return _compile_lib(out, os.path.join(ROOT, "tools", "build", "obj_stamps"), defines=["LMPC_STAMPS"])
 
 
 def build_variant(tag: str, defines, force: bool = False, flags=()) -> str:
@@ -119,11 +119,7 @@ def build_variant(tag: str, defines, force: bool = False, flags=()) -> str:
     out = os.path.join(ROOT, "tools", "build", f"liblmpc_{tag}.so")
     if not force and not _stale(out, srcs + [os.path.join(CSRC, h) for h in HEADERS]):
         return out
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out] + HIP_FLAGS + list(flags) + [f"-D{d}" for d in defines] + srcs
-    subprocess.run(cmd, check=True)
-    return out
+    return _compile_lib(out, os.path.join(ROOT, "tools", "build", f"obj_{tag}"), defines=defines, flags=flags)
 
 
 def build_cpp_test(force: bool = False) -> str:
