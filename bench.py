@@ -41,6 +41,8 @@ def parse():
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
                     help="dense-path kernel (lmpc_set_dense_path); default: gi for config 4, ipm otherwise")
+    ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
+                    help="set an lmpc_options field for this run (A/B of solver settings; the line records it)")
     return ap.parse_args()
 
 
@@ -124,6 +126,13 @@ def main():
     # --dense overrides it.
     dense = args.dense or ("gi" if args.config == 4 else "ipm")
     solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank, dense_path=dense)
+    opts = {}
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        opts[k] = float(v) if any(ch in v for ch in ".e") else int(v)
+    if opts:
+        from legged_mpc_control_amd.solver import solver_options
+        solver.set_options(solver_options(**opts))
     seed = synth.BASE_SEED + args.config
     d_cmd = solver.synth_commands_device(synth.config_cfg(args.config), B, seed, first_index=first, device=dev)
     d_nrm = solver.synth_normals_device(B, seed, first_index=first, device=dev) if terrain else None
@@ -328,6 +337,7 @@ def main():
                 "gait": "mixed" if cfg["gait"] < 0 else ["trot", "crawl", "trot_with_stand", "stand"][cfg["gait"]],
                 "terrain": f"per-leg normals, tilt U(0, {synth.TERRAIN_THETA_MAX}) rad" if terrain else None,
                 "parallelism": f"dp{world} (independent QP shards, no collective)",
+                **({"options": opts} if opts else {}),
             },
             "roofline": {
                 # fp64 compute, not HBM; the counters show fp64 VALU work issued by a latency-bound wave (one

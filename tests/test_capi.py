@@ -120,7 +120,7 @@ def test_options_defaults_and_no_environment_overrides():
     from legged_mpc_control_amd import solver_options
 
     o = solver_options()
-    assert (o.max_iter, o.max_rounds, o.max_attempts) == (40, 4, 3)
+    assert (o.max_iter, o.max_rounds, o.max_attempts) == (40, 8, 3)
     assert (o.gi_max_steps, o.dense_iter_cap, o.dense_polish_iter, o.warm_rounds) == (240, 0, 40, 12)
     assert solver_options(gi_max_steps=20).gi_max_steps == 20
     with pytest.raises(AttributeError):
