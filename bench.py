@@ -41,6 +41,8 @@ def parse():
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
                     help="dense-path kernel (lmpc_set_dense_path); default: gi for config 4, ipm otherwise")
+    ap.add_argument("--index-offset", type=int, default=0,
+                    help="shift the global instance indices (robustness checks on other samples; recorded in config)")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="set an lmpc_options field for this run (A/B of solver settings; the line records it)")
     return ap.parse_args()
@@ -113,6 +115,7 @@ def main():
     else:
         B = args.batch if args.batch is not None else cfg["batch"]
         first, _ = D.shard_range(rank, world, B)
+    first += args.index_offset
     p = synth.params(cfg["robot"])
     terrain = args.config == 4 and not args.flat  # config 4: terrain normals
     wl_name = cfg["name"] + ("+terrain" if terrain else "")
@@ -338,6 +341,7 @@ def main():
                 "terrain": f"per-leg normals, tilt U(0, {synth.TERRAIN_THETA_MAX}) rad" if terrain else None,
                 "parallelism": f"dp{world} (independent QP shards, no collective)",
                 **({"options": opts} if opts else {}),
+                **({"index_offset": args.index_offset} if args.index_offset else {}),
             },
             "roofline": {
                 # fp64 compute, not HBM; the counters show fp64 VALU work issued by a latency-bound wave (one

@@ -94,7 +94,7 @@ typedef struct lmpc_options {
     int max_iter;     /* IPM iterations cap per attempt (default 40) */
     int max_rounds;   /* active-set polish rounds per attempt (default 8) */
     int max_attempts; /* IPM+polish attempts; tol_mu x1e-3 each retry (default 3) */
-    double tol_mu;    /* IPM stop: mean complementarity (default 1e-6) */
+    double tol_mu;    /* IPM stop: mean complementarity, then the polish (default 1e-4) */
     double tol_p;     /* polish primal feasibility, relative to f_max (default 1e-9) */
     double tol_d;     /* polish multiplier sign, relative to gradient scale (default 1e-9) */
     /* ABI 5: the dense paths' caps and the warm-start budget (were environment hooks).  None of them

@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 if (st) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i)
-                        if (z[i] > s[i]) act |= 1 << i;
+                        if (z[i] > LMPC_ACT_RATIO * s[i]) act |= 1 << i;
                     const double fm = fmax(fabs(f[0]), fmax(fabs(f[1]), fabs(f[2])));
                     if (fm < 1e-6 * fzmax) act = 15;
                 }
@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             DSTAMP(8);  // predictor step length + corrector terms
         } else if (mode == CORR) {
             double ds[5], dz[5];
-            double amax = 1.0;
+            double amax = 1.0, dmax = 1.0;  // primal (s) and dual (z) distances to the boundary
 #pragma unroll
             for (int i = 0; i < 5; ++i) ds[i] = dz[i] = 0.0;
             if (st) {
@@ -458,17 +458,22 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                     ds[i] = -o[i] - s[i];
                     dz[i] = (smu - z[i] * s[i] - dsa * dza - z[i] * ds[i]) * is[i];
                     if (ds[i] < 0.0) amax = fmin(amax, -s[i] * __builtin_amdgcn_rcp(ds[i]));
-                    if (dz[i] < 0.0) amax = fmin(amax, -z[i] * __builtin_amdgcn_rcp(dz[i]));
+                    if (dz[i] < 0.0) dmax = fmin(dmax, -z[i] * __builtin_amdgcn_rcp(dz[i]));
                 }
             }
+#if LMPC_SPLIT_STEP
             const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
+            const double alpd = fmin(1.0, LMPC_STEP_FRAC * wave_min(dmax));
+#else
+            const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(fmin(amax, dmax))), alpd = alpha;
+#endif
             if (st) {
 #pragma unroll
                 for (int m = 0; m < 3; ++m) f[m] += alpha * (u[m] - f[m]);
 #pragma unroll
                 for (int i = 0; i < 5; ++i) {
                     s[i] += alpha * ds[i];
-                    z[i] += alpha * dz[i];
+                    z[i] += alpd * dz[i];
                     is[i] = rcp_nr(s[i]);
                 }
             }

@@ -43,12 +43,13 @@ void lmpc_params_a1(lmpc_params* p) {
 
 void lmpc_options_default(lmpc_options* o) {
     o->max_iter = 40;
-    // Hand-over to the polish at a mean complementarity of 1e-6 (was 1e-8): 1.3 fewer interior-point
-    // iterations for 0.6 more polish rounds, the same verified optimum; the larger polish budget keeps
-    // the QPs that need 5-8 rounds off the retry (tools/ab_tol.sh: config 2 -5.5 %, 3-5 -4..-7 %).
+    // Hand-over to the polish at a mean complementarity of 1e-4 (was 1e-8 until round 3): with the faces
+    // classified active where z > 1e-3 s (LMPC_ACT_RATIO) the polish verifies in 1.1-1.5 rounds on average,
+    // so the interior point stops ~3 iterations earlier for the same verified optimum; the polish budget of
+    // 8 rounds keeps the rare QP that needs 5-8 off the retry (tools/ab_opts.sh, profiles/r03/handover/).
     o->max_rounds = 8;
     o->max_attempts = 3;
-    o->tol_mu = 1e-6;
+    o->tol_mu = 1e-4;
     o->tol_p = 1e-9;
     o->tol_d = 1e-9;
     o->gi_max_steps = 240;

@@ -19,6 +19,21 @@ constexpr int LMPC_WAVE = 64;
 #ifndef LMPC_STEP_FRAC
 #define LMPC_STEP_FRAC 0.99
 #endif
+// Hand-over to the polish: a face is guessed active where z > LMPC_ACT_RATIO * s.  At the hand-over
+// (mean complementarity 1e-6) an active face has z/s ~ z^2/mu >> 1 and an inactive one ~ mu/s^2 << 1; the
+// faces in between are near-degenerate, and guessing them active costs fewer polish rounds than guessing
+// them inactive (a wrong active face leaves in the same round a missing one would enter; missing faces
+// enter one per leg-step per round).  numpy replica (tools/polish_guess_proto.py, 1280 config-2 QPs):
+// 1.91 -> 1.13 polish rounds per QP at 1e-3 against the z > s rule.
+// Corrector step: separate primal (f, s) and dual (z) step lengths, each LMPC_STEP_FRAC of its distance to the
+// boundary (0: one common step).  numpy replica (tools/polish_guess_proto.py, 512 config-2 QPs at the 1e-5
+// hand-over): 6.49 -> 6.09 interior-point iterations per QP, modelled slowest QP -8 %.
+#ifndef LMPC_SPLIT_STEP
+#define LMPC_SPLIT_STEP 1
+#endif
+#ifndef LMPC_ACT_RATIO
+#define LMPC_ACT_RATIO 1e-3
+#endif
 #define LMPC_SYNC()                                              \
     do {                                                         \
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \

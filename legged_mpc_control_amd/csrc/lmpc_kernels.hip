@@ -1118,14 +1118,14 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                         for (int i = 0; i < 5; ++i) loc += s[t][i] * z[t][i];
                 mu_c = wave_sum(loc) / mc;
                 if (mu_c < tol || ipm_it >= it_end) {
-                    // active set from the interior point: z > s, lift-off legs -> apex
+                    // active set from the interior point: z > LMPC_ACT_RATIO s, lift-off legs -> apex
 #pragma unroll
                     for (int t = 0; t < LS; ++t) {
                         act[t] = 0;
                         if (!st[t]) continue;
 #pragma unroll
                         for (int i = 0; i < 5; ++i)
-                            if (z[t][i] > s[t][i]) act[t] |= 1 << i;
+                            if (z[t][i] > LMPC_ACT_RATIO * s[t][i]) act[t] |= 1 << i;
                         const double fm = fmax(fabs(f[t][0]), fmax(fabs(f[t][1]), fabs(f[t][2])));
                         if (fm < 1e-6 * fzmax) act[t] = 15;
                     }
@@ -1259,7 +1259,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                 SUB(17);  // (diagnostic) predictor post-step
             } else if (mode == CORR) {
                 double ds[LS][5], dz[LS][5];
-                double amax = 1.0;
+                double amax = 1.0, dmax = 1.0;  // primal (s) and dual (z) distances to the boundary
 #pragma unroll
                 for (int t = 0; t < LS; ++t) {
 #pragma unroll
@@ -1276,10 +1276,15 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                         ds[t][i] = -o[i] - s[t][i];
                         dz[t][i] = (smu - z[t][i] * s[t][i] - dsa * dza - z[t][i] * ds[t][i]) * is;
                         if (ds[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(ds[t][i]));
-                        if (dz[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dz[t][i]));
+                        if (dz[t][i] < 0.0) dmax = fmin(dmax, -z[t][i] * __builtin_amdgcn_rcp(dz[t][i]));
                     }
                 }
+#if LMPC_SPLIT_STEP
                 const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
+                const double alpd = fmin(1.0, LMPC_STEP_FRAC * wave_min(dmax));
+#else
+                const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(fmin(amax, dmax))), alpd = alpha;
+#endif
 #pragma unroll
                 for (int t = 0; t < LS; ++t) {
                     if (!st[t]) continue;
@@ -1288,7 +1293,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
 #pragma unroll
                     for (int i = 0; i < 5; ++i) {
                         s[t][i] += alpha * ds[t][i];
-                        z[t][i] += alpha * dz[t][i];
+                        z[t][i] += alpd * dz[t][i];
                     }
                 }
                 ++ipm_it;

@@ -89,6 +89,8 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
         elif rule == "split":
             ap = min(1.0, 0.99 * step(s, ds))
             ad = min(1.0, 0.99 * step(z, dz))
+        elif rule.startswith("frac"):  # fixed fraction to the boundary, e.g. frac0.995
+            ap = ad = min(1.0, float(rule[4:]) * min(step(s, ds), step(z, dz)))
         else:
             frac = 0.99 if rule == "same" else 1.0 - min(0.01, mu)
             ap = ad = min(1.0, frac * min(step(s, ds), step(z, dz)))
