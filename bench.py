@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
-                    help="dense-path kernel (lmpc_set_dense_path); default: gi for config 4, ipm otherwise")
+                    help="dense-path kernel (lmpc_set_dense_path); default ipm")
     ap.add_argument("--index-offset", type=int, default=0,
                     help="shift the global instance indices (robustness checks on other samples; recorded in config)")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
@@ -123,11 +123,10 @@ def main():
     # Inputs are generated ON THE DEVICE from (seed, global index): every rank builds its own shard in
     # HBM, no input bytes cross PCIe or xGMI.  Commands -> records + contact schedules
     # by the expansion kernel (8f-1); the timed step below is the QP solve over those records.
-    # Dense-path kernel per workload (fixed per context, so no answer depends on it): the interior point when every
-    # SIMD holds about one QP and the launch waits for the slowest (configs 2/3/5), the dual active set -- half the
-    # mean cost, a longer tail -- when each SIMD streams through many QPs (config 4: 64 per SIMD); DESIGN.md 4b.
-    # --dense overrides it.
-    dense = args.dense or ("gi" if args.config == 4 else "ipm")
+    # Dense-path kernel: the interior point for every workload since the round-3 hand-over rework (DESIGN.md 2.4;
+    # config 4 13.8 ms against 15.1 ms on the dual active set, profiles/r03/handover/ab_c4_dense.log).  Fixed per
+    # context, so no answer depends on it; --dense overrides it.
+    dense = args.dense or "ipm"
     solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank, dense_path=dense)
     opts = {}
     for kv in args.opt:
@@ -293,7 +292,7 @@ def main():
     executed = None
     # the committed PMC figures are keyed by workload, plus "/<mode>" when --dense overrides the config's own path
     # (configs 3 and 5 run the Riccati kernel by default: H > 16 has no dense path)
-    overridden = args.dense is not None and args.dense != ("gi" if args.config == 4 else "ipm")
+    overridden = args.dense is not None and args.dense != "ipm"
     wl = (f"{wl_name}/{mode}" if overridden else wl_name) if args.batch is None else None
     try:
         tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))

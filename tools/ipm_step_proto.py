@@ -67,7 +67,7 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
         dz = (smu - z * s - dsa * dza - z * ds) / s
         df = u - f
         if rule.startswith("gondzio"):  # multiple centrality correctors (Colombo & Gondzio), same factorisation
-            kmax = int(rule[7:] or 2)
+            kmax = int(rule[7:].rstrip("s") or 2)
             a0 = min(step(s, ds), step(z, dz))
             for _ in range(kmax):
                 at = min(1.0, 1.5 * a0 + 0.1)
@@ -85,7 +85,10 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
                 else:
                     CORR[1] += 1
                     break
-            ap = ad = min(1.0, 0.99 * a0)
+            if rule.endswith("s"):  # gondzioNs: correctors, then separate primal / dual step lengths
+                ap, ad = min(1.0, 0.99 * step(s, ds)), min(1.0, 0.99 * step(z, dz))
+            else:
+                ap = ad = min(1.0, 0.99 * a0)
         elif rule == "split":
             ap = min(1.0, 0.99 * step(s, ds))
             ad = min(1.0, 0.99 * step(z, dz))
