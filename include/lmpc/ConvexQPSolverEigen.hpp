@@ -55,7 +55,7 @@ public:
         act_.assign((size_t)4 * H_, 0);
         act_in_.assign((size_t)4 * H_, 0);
         error_ = lmpc_create(&params_, H_, 1, device_, &ctx_);
-        if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_GI);
+        if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_IPM);
     }
     ~ConvexQPSolver() { lmpc_destroy(ctx_); }
     ConvexQPSolver(const ConvexQPSolver&) = delete;

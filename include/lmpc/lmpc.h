@@ -126,9 +126,9 @@ int lmpc_set_options(lmpc_ctx* ctx, const lmpc_options* o);
 int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
 
 /* Dense path (ABI 3).  QPs with 1..20 stance leg-steps at H <= 16 are solved on the condensed QP by
- * LMPC_DENSE_IPM (interior point + active-set polish; the default: fastest when every SIMD holds one QP
- * and the launch waits for its slowest, e.g. 1024 QPs) or LMPC_DENSE_GI (dual active set: about half
- * the mean cost per QP, a longer tail -- the choice for one QP per call, e.g. the per-tick drop-in);
+ * LMPC_DENSE_IPM (interior point + active-set polish; the default and, since round 3, the faster kernel
+ * both for large batches and for one QP per call, e.g. the per-tick drop-in) or LMPC_DENSE_GI (dual active
+ * set: one factorisation, then rank-one steps; a long tail of many-step QPs);
  * LMPC_DENSE_OFF sends every QP to the Riccati kernel.  All return the same optimum: a dense QP left
  * without a verified optimum (iteration or step cap, non-finite iterate) is solved by the Riccati
  * kernel in the same call, so its status is the Riccati kernel's.  Set it before

@@ -25,9 +25,11 @@ ConvexQPSolver::ConvexQPSolver(const double* q_weights, const double* r_weights,
     error_ = lmpc_create(&params_, H_, 1, device, &ctx_);
     // Warm start is on by default (set_warm_start): every tick then runs on the Riccati kernel, from the
     // previous tick's verified active set (the first tick from the cold interior point).  Cold solves
-    // (set_warm_start(false)) take the dual active set, the lower-latency dense kernel for one QP per call.
-    // The Python drop-in (legged_mpc_control_amd.ConvexQPSolver) has the same defaults.
-    if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_GI);
+    // (set_warm_start(false)) take the condensed interior point, since round 3 the lower-latency dense kernel
+    // for one QP per call too (0.146 ms mean / 0.183 ms p99 per call at H = 10 against 0.166 / 0.303 on the dual
+    // active set, tools/single_qp_latency.py).  The Python drop-in (legged_mpc_control_amd.ConvexQPSolver) has
+    // the same defaults.
+    if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_IPM);
 }
 
 ConvexQPSolver::~ConvexQPSolver() { lmpc_destroy(ctx_); }

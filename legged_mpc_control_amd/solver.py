@@ -375,9 +375,9 @@ class ConvexQPSolver:
         self._p = p
         # Same defaults as the C++ drop-in (legged::ConvexQPSolver): warm start on, so every tick runs on the
         # Riccati kernel from the previous tick's verified active set shifted one step (the reference's OSQP
-        # warm-starts too, ConvexQPSolver.cpp:185); cold solves (set_warm_start(False)) take the dual active
-        # set, the lower-latency dense kernel for one QP per call.
-        self._dev = BatchedConvexQPSolver(p, self.H, 1, device, dense_path="gi")
+        # warm-starts too, ConvexQPSolver.cpp:185); cold solves (set_warm_start(False)) take the condensed
+        # interior point, since round 3 also the lower-latency dense kernel for one QP per call.
+        self._dev = BatchedConvexQPSolver(p, self.H, 1, device, dense_path="ipm")
         self._rec = np.zeros((1, 33 + 12 * self.H))
         self._con = np.ones((1, self.H, 4), dtype=np.uint8)
         self._warm = True

@@ -456,9 +456,9 @@ def test_dense_path_api(monkeypatch):
     monkeypatch.delenv("LMPC_DENSE")
     p30, H30, _, _ = synth.config_batch(5, count=1)
     assert BatchedConvexQPSolver(p30, H30, max_batch=1, dense_path="gi").dense_path == "off"
-    # the single-QP mirror (ConvexMpc drop-in) runs the dual active set
+    # the single-QP mirror (ConvexMpc drop-in) runs the interior point (round 3: lower latency than the dual active set)
     from legged_mpc_control_amd import ConvexQPSolver
-    assert ConvexQPSolver(p.q_weights, p.r_weights, horizon=10)._dev.dense_path == "gi"
+    assert ConvexQPSolver(p.q_weights, p.r_weights, horizon=10)._dev.dense_path == "ipm"
 
 
 def test_gi_step_cap_hands_over_to_riccati():

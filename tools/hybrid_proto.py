@@ -99,7 +99,18 @@ def polish(Hm, g, act, mu, fmax, max_rounds=12, tol_p=1e-9, tol_d=1e-9, rule="si
                     changed = True
                 continue
             cand = [(o[i], i) for i in range(5) if not (act[b] >> i) & 1 and o[i] > tol_p * fmax]
-            if cand:
+            if cand and rule == "multi":
+                # every violated face in, most violated first, while the active rows stay independent (an
+                # opposite pair is the lift-off apex)
+                new = act[b]
+                for _, i in sorted(cand, reverse=True):
+                    c2 = new | (1 << i)
+                    rows = [k for k in range(5) if (c2 >> k) & 1]
+                    if (c2 & 3) == 3 or (c2 & 12) == 12 or (len(rows) <= 3 and np.linalg.matrix_rank(C[rows]) == len(rows)):
+                        new = c2
+                act[b] = new
+                changed = True
+            elif cand:
                 act[b] |= 1 << max(cand)[1]
                 changed = True
             elif apex[b]:

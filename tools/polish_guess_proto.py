@@ -48,7 +48,8 @@ def main():
             for theta in [float(x) for x in os.environ.get("PG_THETAS", "1,0.1,10").split(",")]:
                 its, rds, bad = [], [], 0
                 for (Hm, g, st, idx), (f, s, z, it) in zip(qps, runs):
-                    _, rd, ok = polish(Hm, g, guess(f, s, z, p.f_max, theta), p.mu, p.f_max, max_rounds=12)
+                    _, rd, ok = polish(Hm, g, guess(f, s, z, p.f_max, theta), p.mu, p.f_max, max_rounds=12,
+                                       rule=os.environ.get("PG_POLISH", "single"))
                     bad += not ok
                     its.append(it)
                     rds.append(rd)
