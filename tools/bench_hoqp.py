@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-sample", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tol-mu", type=float, default=None, help="interior-point stop (lmpc_hoqp_options.tol_mu; A/B)")
     ap.add_argument("--crossover", type=int, default=1, choices=(0, 1),
                     help="lmpc_hoqp_options.crossover (exact active-set step after each level's interior point)")
     return ap.parse_args()
@@ -93,7 +94,7 @@ def main():
     base = np.stack([HQ.pack(c, dims) for c in chains])
     rec = np.ascontiguousarray(np.resize(base, (B, base.shape[1])))
     solver = HQ.HoqpBatch(dims, B, local_rank)
-    solver.set_options(crossover=args.crossover)
+    solver.set_options(crossover=args.crossover, tol_mu=args.tol_mu)
     d_rec = torch.from_numpy(rec).to(dev)
     d_x = torch.empty((B, dims.num_levels, dims.num_vars), dtype=torch.float64, device=dev)
     d_w = torch.empty((B, max(solver.slack_len, 1)), dtype=torch.float64, device=dev)
