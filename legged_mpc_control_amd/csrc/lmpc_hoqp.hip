@@ -773,6 +773,10 @@ __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS
 // (HoQp.cpp:158-174), an active-set method: this makes the degenerate levels exact too.
 constexpr int XO_ROUNDS = 6;
 constexpr double HQ_HFLOOR = 1e-10;  // interior-point margin on exactly tight frozen rows (kernel, below)
+#ifndef LMPC_HQ_XO_TOL
+#define LMPC_HQ_XO_TOL 1e-13
+#endif
+constexpr double HQ_XO_TOL = LMPC_HQ_XO_TOL;  // first-pass interior-point stop ahead of the crossover (two passes)
 template <int NP>
 __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS& S_, int p, int nr, int nd, double bd0,
                                                     double bd1, int fl0, int fl1, double scale, const gdouble* Hg,
@@ -1083,207 +1087,217 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         bool numstop = false;  // left on a non-finite Newton direction
         bool clean = false;    // stopped on the clean criterion (complementarity and residuals within tolerance)
         double mu_last = 0.0, res_last = 0.0;
-        for (;; ++it) {
-            // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
-            double rp1[2], rpg[2], rdv[2];
-            double cs = 0.0, res = 0.0;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int r = lane + 64 * k;
-                rp1[k] = rpg[k] = rdv[k] = 0.0;
-                if (r < nr) {
-                    const double ty = row_dot<NP>(S, ls, nd, r, S.y);
-                    S.q[r] = W.zg[k];
-                    if (r < p) {
-                        rpg[k] = ty + W.sg[k] - W.bd[k];
-                        cs += W.sg[k] * W.zg[k];
-                    } else {
-                        rpg[k] = ty - W.v[k] + W.sg[k] - W.bd[k];
-                        rp1[k] = -W.v[k] + W.s1[k];
-                        rdv[k] = W.v[k] - W.z1[k] - W.zg[k];
-                        cs += W.sg[k] * W.zg[k] + W.s1[k] * W.z1[k];
-                    }
-                    res = nan_max(res, nan_max(fabs(rpg[k]), nan_max(fabs(rp1[k]), fabs(rdv[k]))));
-                }
-            }
-            LMPC_SYNC();
-            double rdy = 0.0;
-            if (lane < nd) {
-                double a = S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
-                a += hy_dot<NP>(P, Hg, S.y, nd, lane);
-                rdy = a;
-                res = nan_max(res, fabs(a));
-            }
-            const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
-            mu_last = mu;
-            res = wave_reduce<OpNanMax>(res);
-            res_last = res;
-            HSTAMP(3);
-            if (!(isfinite(mu) && isfinite(res))) {
-                nonfin = true;
-                break;
-            }
-            // converged; or degenerate (rows whose slack and multiplier both vanish): complementarity 1e3 below
-            // its tolerance while the dual residual stalls within 1e3 of its own, where the huge weights z/s
-            // of those rows leave the Newton directions no more accurate than the iterate already is
-            clean = mu <= P.tol_mu * scale && res <= P.tol_res * scale;
-            if (clean || (mu <= 1e-3 * P.tol_mu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter)
-                break;
-            // weights and K = Hy + R' diag(wh) R
-            double w1[2], wg[2], dl[2], is1[2], isg[2], idl[2];  // weights and the reciprocals both Newton
-#pragma unroll                                                        // systems divide by
-            for (int k = 0; k < 2; ++k) {
-                const int r = lane + 64 * k;
-                is1[k] = 1.0 / W.s1[k];
-                isg[k] = 1.0 / W.sg[k];
-                w1[k] = W.z1[k] * is1[k];
-                wg[k] = W.zg[k] * isg[k];
-                dl[k] = 1.0 + w1[k] + wg[k];
-                idl[k] = 1.0 / dl[k];
-                if (r < P.rmax) S.wh[r] = r >= nr ? 0.0 : (r < p ? wg[k] : wg[k] * (1.0 + w1[k]) * idl[k]);
-            }
-            LMPC_SYNC();
-            form_K(P, S, nr, nd, Hg, lane);
-            HSTAMP(4);
-            chol_floor<NP>(S, ls, nd, lane);
-            HSTAMP(5);
-            // Newton system for a complementarity target rc (per row): returns dy (lane j) and per-row
-            // directions; dz = W C dx + (z r_p - rc)/s, (H + C'WC) dx = -r_d - C'(z r_p - rc)/s
-            double ds1[2], dsg[2], dz1[2], dzg[2], dv[2];
-            auto newton = [&](const double rc1[2], const double rcg[2]) {
-                HQSUB_START();
-                double rv[2];
+        // Two passes (round 3): with the crossover on, the interior point first stops at HQ_XO_TOL (or tol_mu, if
+        // looser) and hands its iterate to the crossover; only a level whose crossover does not verify resumes the
+        // interior point from that iterate down to tol_mu and tries the crossover again.  The verified answer is
+        // the active-set optimum either way (tools/hoqp_tol_ab.sh: 4.81 -> 3.89 ms per 4096 WBC chains at 1e-7).
+        const bool two_pass = P.crossover && P.tol_mu < HQ_XO_TOL;
+        bool exact = false;
+        int xo = 0;  // iteration word bits 16-17: 1 crossover tried, 2 verified and taken
+        for (int pass = two_pass ? 0 : 1; pass < 2; ++pass) {
+            const double tmu = pass == 0 ? HQ_XO_TOL : P.tol_mu;
+            for (;; ++it) {
+                // residuals: r_d = H x + c + C'z, r_p = C x + slack - d
+                double rp1[2], rpg[2], rdv[2];
+                double cs = 0.0, res = 0.0;
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int r = lane + 64 * k;
-                    rv[k] = 0.0;
+                    rp1[k] = rpg[k] = rdv[k] = 0.0;
                     if (r < nr) {
-                        const double eg = (W.zg[k] * rpg[k] - rcg[k]) * isg[k];
+                        const double ty = row_dot<NP>(S, ls, nd, r, S.y);
+                        S.q[r] = W.zg[k];
                         if (r < p) {
-                            S.q[r] = -eg;
+                            rpg[k] = ty + W.sg[k] - W.bd[k];
+                            cs += W.sg[k] * W.zg[k];
                         } else {
-                            const double e1 = (W.z1[k] * rp1[k] - rc1[k]) * is1[k];
-                            rv[k] = -rdv[k] + e1 + eg;
-                            S.q[r] = -eg + wg[k] * rv[k] * idl[k];
+                            rpg[k] = ty - W.v[k] + W.sg[k] - W.bd[k];
+                            rp1[k] = -W.v[k] + W.s1[k];
+                            rdv[k] = W.v[k] - W.z1[k] - W.zg[k];
+                            cs += W.sg[k] * W.zg[k] + W.s1[k] * W.z1[k];
                         }
+                        res = nan_max(res, nan_max(fabs(rpg[k]), nan_max(fabs(rp1[k]), fabs(rdv[k]))));
                     }
                 }
                 LMPC_SYNC();
-                HQSUB(0);
-                const double rhs = lane < nd ? -rdy + rt_dot(S, ls, nr, S.q, lane) : 0.0;
-                HQSUB(1);
-                chol_solve<NP>(S, ls, nd, rhs, S.dy, lane);
-                HQSUB(2);
+                double rdy = 0.0;
+                if (lane < nd) {
+                    double a = S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
+                    a += hy_dot<NP>(P, Hg, S.y, nd, lane);
+                    rdy = a;
+                    res = nan_max(res, fabs(a));
+                }
+                const double mu = mc > 0.0 ? wave_sum(cs) / mc : 0.0;
+                mu_last = mu;
+                res = wave_reduce<OpNanMax>(res);
+                res_last = res;
+                HSTAMP(3);
+                if (!(isfinite(mu) && isfinite(res))) {
+                    nonfin = true;
+                    break;
+                }
+                // converged; or degenerate (rows whose slack and multiplier both vanish): complementarity 1e3 below
+                // its tolerance while the dual residual stalls within 1e3 of its own, where the huge weights z/s
+                // of those rows leave the Newton directions no more accurate than the iterate already is
+                clean = mu <= tmu * scale && res <= P.tol_res * scale;
+                if (clean || (mu <= 1e-3 * tmu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter)
+                    break;
+                // weights and K = Hy + R' diag(wh) R
+                double w1[2], wg[2], dl[2], is1[2], isg[2], idl[2];  // weights and the reciprocals both Newton
+#pragma unroll                                                        // systems divide by
+                for (int k = 0; k < 2; ++k) {
+                    const int r = lane + 64 * k;
+                    is1[k] = 1.0 / W.s1[k];
+                    isg[k] = 1.0 / W.sg[k];
+                    w1[k] = W.z1[k] * is1[k];
+                    wg[k] = W.zg[k] * isg[k];
+                    dl[k] = 1.0 + w1[k] + wg[k];
+                    idl[k] = 1.0 / dl[k];
+                    if (r < P.rmax) S.wh[r] = r >= nr ? 0.0 : (r < p ? wg[k] : wg[k] * (1.0 + w1[k]) * idl[k]);
+                }
+                LMPC_SYNC();
+                form_K(P, S, nr, nd, Hg, lane);
+                HSTAMP(4);
+                chol_floor<NP>(S, ls, nd, lane);
+                HSTAMP(5);
+                // Newton system for a complementarity target rc (per row): returns dy (lane j) and per-row
+                // directions; dz = W C dx + (z r_p - rc)/s, (H + C'WC) dx = -r_d - C'(z r_p - rc)/s
+                double ds1[2], dsg[2], dz1[2], dzg[2], dv[2];
+                auto newton = [&](const double rc1[2], const double rcg[2]) {
+                    HQSUB_START();
+                    double rv[2];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int r = lane + 64 * k;
+                        rv[k] = 0.0;
+                        if (r < nr) {
+                            const double eg = (W.zg[k] * rpg[k] - rcg[k]) * isg[k];
+                            if (r < p) {
+                                S.q[r] = -eg;
+                            } else {
+                                const double e1 = (W.z1[k] * rp1[k] - rc1[k]) * is1[k];
+                                rv[k] = -rdv[k] + e1 + eg;
+                                S.q[r] = -eg + wg[k] * rv[k] * idl[k];
+                            }
+                        }
+                    }
+                    LMPC_SYNC();
+                    HQSUB(0);
+                    const double rhs = lane < nd ? -rdy + rt_dot(S, ls, nr, S.q, lane) : 0.0;
+                    HQSUB(1);
+                    chol_solve<NP>(S, ls, nd, rhs, S.dy, lane);
+                    HQSUB(2);
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int r = lane + 64 * k;
+                        ds1[k] = dsg[k] = dz1[k] = dzg[k] = dv[k] = 0.0;
+                        if (r < nr) {
+                            const double td = row_dot<NP>(S, ls, nd, r, S.dy);
+                            double cg = td;
+                            if (r >= p) {
+                                dv[k] = (rv[k] + wg[k] * td) * idl[k];
+                                cg = td - dv[k];
+                                ds1[k] = -rp1[k] + dv[k];
+                                dz1[k] = (-rc1[k] - W.z1[k] * ds1[k]) * is1[k];
+                            }
+                            dsg[k] = -rpg[k] - cg;
+                            dzg[k] = (-rcg[k] - W.zg[k] * dsg[k]) * isg[k];
+                        }
+                    }
+                    HQSUB(3);
+                };
+                auto max_step = [&]() {
+                    double a = 1.0;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int r = lane + 64 * k;
+                        if (r < nr) {
+                            if (dsg[k] < 0.0) a = fmin(a, -W.sg[k] / dsg[k]);
+                            if (dzg[k] < 0.0) a = fmin(a, -W.zg[k] / dzg[k]);
+                            if (r >= p) {
+                                if (ds1[k] < 0.0) a = fmin(a, -W.s1[k] / ds1[k]);
+                                if (dz1[k] < 0.0) a = fmin(a, -W.z1[k] / dz1[k]);
+                            }
+                        }
+                    }
+                    return wave_min(a);
+                };
+                double rc1[2], rcg[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    rc1[k] = W.s1[k] * W.z1[k];
+                    rcg[k] = W.sg[k] * W.zg[k];
+                }
+                newton(rc1, rcg);
+                const double a_aff = max_step();
+                HQSUB(4);
+                double ca = 0.0;
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int r = lane + 64 * k;
-                    ds1[k] = dsg[k] = dz1[k] = dzg[k] = dv[k] = 0.0;
                     if (r < nr) {
-                        const double td = row_dot<NP>(S, ls, nd, r, S.dy);
-                        double cg = td;
-                        if (r >= p) {
-                            dv[k] = (rv[k] + wg[k] * td) * idl[k];
-                            cg = td - dv[k];
-                            ds1[k] = -rp1[k] + dv[k];
-                            dz1[k] = (-rc1[k] - W.z1[k] * ds1[k]) * is1[k];
-                        }
-                        dsg[k] = -rpg[k] - cg;
-                        dzg[k] = (-rcg[k] - W.zg[k] * dsg[k]) * isg[k];
+                        ca += (W.sg[k] + a_aff * dsg[k]) * (W.zg[k] + a_aff * dzg[k]);
+                        if (r >= p) ca += (W.s1[k] + a_aff * ds1[k]) * (W.z1[k] + a_aff * dz1[k]);
                     }
                 }
-                HQSUB(3);
-            };
-            auto max_step = [&]() {
-                double a = 1.0;
+                const double mu_aff = mc > 0.0 ? wave_sum(ca) / mc : 0.0;
+                const double sig = mu > 0.0 ? (mu_aff / mu) * (mu_aff / mu) * (mu_aff / mu) * mu : 0.0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    rc1[k] = W.s1[k] * W.z1[k] + ds1[k] * dz1[k] - sig;
+                    rcg[k] = W.sg[k] * W.zg[k] + dsg[k] * dzg[k] - sig;
+                }
+                HQSUB(5);
+                newton(rc1, rcg);
+                const double a = fmin(1.0, HQ_FRAC * max_step());
+                HQSUB(4);
+                // a non-finite direction (weights z/s overflowing as a degenerate level's slacks reach the bottom
+                // of the double range) ends the level on the current iterate, which is kept
+                bool fin = isfinite(a) && (lane >= nd || isfinite((double)S.dy[lane]));
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+                    fin = fin && isfinite(dv[k]) && isfinite(ds1[k]) && isfinite(dz1[k]) && isfinite(dsg[k]) &&
+                          isfinite(dzg[k]);
+                if (__ballot(!fin)) {
+                    numstop = true;
+                    break;
+                }
+                if (lane < nd) S.y[lane] += a * S.dy[lane];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    W.v[k] += a * dv[k];
+                    W.s1[k] += a * ds1[k];
+                    W.z1[k] += a * dz1[k];
+                    W.sg[k] += a * dsg[k];
+                    W.zg[k] += a * dzg[k];
+                }
+                LMPC_SYNC();
+                HQSUB(6);
+                HSTAMP(6);
+            }
+            // the exact crossover on the identified active set, taken when it verifies: the clean stop's residual
+            // tolerance (1e-7 of the scale by default) is far looser than the active-set answer
+            if (P.crossover && !nonfin && nr > 0 && nd > 0) {
+                int fl[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int r = lane + 64 * k;
-                    if (r < nr) {
-                        if (dsg[k] < 0.0) a = fmin(a, -W.sg[k] / dsg[k]);
-                        if (dzg[k] < 0.0) a = fmin(a, -W.zg[k] / dzg[k]);
-                        if (r >= p) {
-                            if (ds1[k] < 0.0) a = fmin(a, -W.s1[k] / ds1[k]);
-                            if (dz1[k] < 0.0) a = fmin(a, -W.z1[k] / dz1[k]);
-                        }
-                    }
+                    fl[k] = 0;
+                    if (r < p) fl[k] = W.zg[k] > W.sg[k] ? 1 : 0;
+                    else if (r < nr) fl[k] = W.zg[k] > W.sg[k] ? 2 : 0;
                 }
-                return wave_min(a);
-            };
-            double rc1[2], rcg[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                rc1[k] = W.s1[k] * W.z1[k];
-                rcg[k] = W.sg[k] * W.zg[k];
+                exact = crossover<NP>(P, S, p, nr, nd, hb_true[0], hb_true[1], fl[0], fl[1], scale, Hg, Tg, lane);
+                xo = exact ? 3 : 1;
+                any_exact = any_exact || exact;
             }
-            newton(rc1, rcg);
-            const double a_aff = max_step();
-            HQSUB(4);
-            double ca = 0.0;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int r = lane + 64 * k;
-                if (r < nr) {
-                    ca += (W.sg[k] + a_aff * dsg[k]) * (W.zg[k] + a_aff * dzg[k]);
-                    if (r >= p) ca += (W.s1[k] + a_aff * ds1[k]) * (W.z1[k] + a_aff * dz1[k]);
-                }
-            }
-            const double mu_aff = mc > 0.0 ? wave_sum(ca) / mc : 0.0;
-            const double sig = mu > 0.0 ? (mu_aff / mu) * (mu_aff / mu) * (mu_aff / mu) * mu : 0.0;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                rc1[k] = W.s1[k] * W.z1[k] + ds1[k] * dz1[k] - sig;
-                rcg[k] = W.sg[k] * W.zg[k] + dsg[k] * dzg[k] - sig;
-            }
-            HQSUB(5);
-            newton(rc1, rcg);
-            const double a = fmin(1.0, HQ_FRAC * max_step());
-            HQSUB(4);
-            // a non-finite direction (weights z/s overflowing as a degenerate level's slacks reach the bottom
-            // of the double range) ends the level on the current iterate, which is kept
-            bool fin = isfinite(a) && (lane >= nd || isfinite((double)S.dy[lane]));
-#pragma unroll
-            for (int k = 0; k < 2; ++k)
-                fin = fin && isfinite(dv[k]) && isfinite(ds1[k]) && isfinite(dz1[k]) && isfinite(dsg[k]) &&
-                      isfinite(dzg[k]);
-            if (__ballot(!fin)) {
-                numstop = true;
-                break;
-            }
-            if (lane < nd) S.y[lane] += a * S.dy[lane];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                W.v[k] += a * dv[k];
-                W.s1[k] += a * ds1[k];
-                W.z1[k] += a * dz1[k];
-                W.sg[k] += a * dsg[k];
-                W.zg[k] += a * dzg[k];
-            }
-            LMPC_SYNC();
-            HQSUB(6);
-            HSTAMP(6);
-        }
-        // the exact crossover on the identified active set, taken when it verifies: the clean stop's residual
-        // tolerance (1e-7 of the scale by default) is far looser than the active-set answer
-        bool exact = false;
-        int xo = 0;  // iteration word bits 16-17: 1 crossover tried, 2 verified and taken
-        if (P.crossover && !nonfin && nr > 0 && nd > 0) {
-            int fl[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int r = lane + 64 * k;
-                fl[k] = 0;
-                if (r < p) fl[k] = W.zg[k] > W.sg[k] ? 1 : 0;
-                else if (r < nr) fl[k] = W.zg[k] > W.sg[k] ? 2 : 0;
-            }
-            exact = crossover<NP>(P, S, p, nr, nd, hb_true[0], hb_true[1], fl[0], fl[1], scale, Hg, Tg, lane);
-            xo = exact ? 3 : 1;
-            any_exact = any_exact || exact;
+            // resume only from a finite iterate that stopped on its criterion (not the cap, not a non-finite direction)
+            if (exact || nonfin || numstop || it >= P.max_iter || !(nr > 0 && nd > 0)) break;
         }
         exact = exact || clean;
         // LMPC_QP_CONVERGED: the clean stop, a verified crossover, or -- documented in lmpc_hoqp.h -- the relaxed
         // degenerate stop (complementarity 1e3 below its tolerance, residuals within 1e3 of theirs); a level left on
         // the iteration cap or on a non-finite direction short of that reports LMPC_QP_MAX_ITER
-        const bool relaxed = mu_last <= 1e-3 * P.tol_mu * scale && res_last <= 1e3 * P.tol_res * scale;
+        const bool relaxed = mu_last <= 1e-3 * P.tol_mu * scale && res_last <= 1e3 * P.tol_res * scale;  // final pass
         if (!exact && (it >= P.max_iter || (numstop && !relaxed))) st = 1;
         if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16);
         // ---- outputs: w_l = max(0, D_l Z y - g) for the final y, x += Z y ------------------------------
