@@ -774,7 +774,7 @@ __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS
 constexpr int XO_ROUNDS = 6;
 constexpr double HQ_HFLOOR = 1e-10;  // interior-point margin on exactly tight frozen rows (kernel, below)
 #ifndef LMPC_HQ_XO_TOL
-#define LMPC_HQ_XO_TOL 1e-13
+#define LMPC_HQ_XO_TOL 1e-9
 #endif
 constexpr double HQ_XO_TOL = LMPC_HQ_XO_TOL;  // first-pass interior-point stop ahead of the crossover (two passes)
 template <int NP>
@@ -1090,7 +1090,10 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         // Two passes (round 3): with the crossover on, the interior point first stops at HQ_XO_TOL (or tol_mu, if
         // looser) and hands its iterate to the crossover; only a level whose crossover does not verify resumes the
         // interior point from that iterate down to tol_mu and tries the crossover again.  The verified answer is
-        // the active-set optimum either way (tools/hoqp_tol_ab.sh: 4.81 -> 3.89 ms per 4096 WBC chains at 1e-7).
+        // the active-set optimum either way.  At 1e-9 every level of the committed WBC golden chains verifies
+        // (4.83 -> 4.43 ms per 4096 WBC chains); at 1e-7 (4.00 ms) one of their 48 levels keeps its iterate
+        // (1.6e-9 off), because the flat-direction components of the exact answers above it change
+        // (tools/hoqp_xo_check.py, profiles/r03/hoqp_2pass/).
         const bool two_pass = P.crossover && P.tol_mu < HQ_XO_TOL;
         bool exact = false;
         int xo = 0;  // iteration word bits 16-17: 1 crossover tried, 2 verified and taken
