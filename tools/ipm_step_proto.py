@@ -60,7 +60,7 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
         dza = -z - W * dsa
         amax = min(step(s, dsa), step(z, dza))
         mu_aff = (s + amax * dsa) @ (z + amax * dza) / m
-        smu = (mu_aff / mu) ** 3 * mu
+        smu = (mu_aff / mu) ** float(os.environ.get("SIGMA_EXP", 3)) * mu
         wv = (z * (s - bvec) + smu - dsa * dza) / s
         u = Kinv @ -(g + C.T @ wv)
         ds = -(C @ u - bvec) - s
@@ -89,9 +89,10 @@ def ipm(Hm, g, st, p, rule="same", tol=1e-8, max_iter=40):
                 ap, ad = min(1.0, 0.99 * step(s, ds)), min(1.0, 0.99 * step(z, dz))
             else:
                 ap = ad = min(1.0, 0.99 * a0)
-        elif rule == "split":
-            ap = min(1.0, 0.99 * step(s, ds))
-            ad = min(1.0, 0.99 * step(z, dz))
+        elif rule.startswith("split"):  # split[frac]: separate primal / dual step lengths (the kernels, round 3)
+            fr = float(rule[5:] or 0.99)
+            ap = min(1.0, fr * step(s, ds))
+            ad = min(1.0, fr * step(z, dz))
         elif rule.startswith("frac"):  # fixed fraction to the boundary, e.g. frac0.995
             ap = ad = min(1.0, float(rule[4:]) * min(step(s, ds), step(z, dz)))
         else:
