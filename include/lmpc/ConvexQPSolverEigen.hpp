@@ -18,8 +18,9 @@
 //
 // Header-only; needs Eigen and the reference headers, so it is compiled only inside that build.  The non-Eigen
 // mirror (ConvexQPSolver.hpp) is what this repository's tests exercise; both call the same C-ABI (lmpc.h) with
-// the same defaults (warm start on, dual active set for cold solves).  tests/cpp/eigen_dropin_test.cpp compiles
-// this header against a minimal test stand-in of the few Eigen and reference members it touches.
+// the same defaults (warm start on, the condensed interior point LMPC_DENSE_IPM for cold solves).
+// tests/cpp/eigen_dropin_test.cpp compiles this header against a minimal test stand-in of the few Eigen and
+// reference members it touches; it has not been compiled against real Eigen (absent from this image).
 #pragma once
 
 #include <Eigen/Dense>
@@ -85,6 +86,10 @@ public:
 
     // ConvexQPSolver.cpp:254-313 (x0, x_ref, v_d_world written back at :260) + :329-346 (bounds)
     void calc_mpc_reference(LeggedState& state, LeggedContactFSM leg_FSM[NUM_LEG]) {
+        if (!ctx_ || H_ == 0) {  // default-constructed (or moved-from) solver: no buffers to write into
+            error_ = LMPC_ERR_ARG;
+            return;
+        }
         lmpc_state_in st;
         for (int i = 0; i < 3; ++i) {
             st.root_euler[i] = state.fbk.root_euler[i];
@@ -103,7 +108,7 @@ public:
         params_.robot_mass = state.param.robot_mass;
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) params_.trunk_inertia[3 * i + j] = state.param.a1_trunk_inertia(i, j);
-        if (ctx_) (void)lmpc_set_params(ctx_, &params_);
+        (void)lmpc_set_params(ctx_, &params_);
         double vdw[3];
         lmpc_pack_record(&params_, H_, &st, rec_.data(), vdw);
         for (int i = 0; i < 3; ++i) state.ctrl.root_lin_vel_d_world[i] = vdw[i];
@@ -115,6 +120,10 @@ public:
 
     // ConvexQPSolver.cpp:329-346: step 0 from plan_contacts, step i from the reference FSM's own prediction
     void update_bound_constraints(bool contacts[NUM_LEG], LeggedContactFSM leg_FSM[NUM_LEG]) {
+        if (!ctx_ || H_ == 0 || contact_.size() < (size_t)4 * H_) {
+            error_ = LMPC_ERR_ARG;
+            return;
+        }
         for (int j = 0; j < NUM_LEG; ++j) contact_[j] = contacts[j] ? 1 : 0;
         for (int i = 1; i < H_; ++i)
             for (int j = 0; j < NUM_LEG; ++j)

@@ -93,7 +93,8 @@ typedef struct lmpc_params {
 typedef struct lmpc_options {
     int max_iter;     /* IPM iterations cap per attempt (default 40) */
     int max_rounds;   /* active-set polish rounds per attempt (default 8) */
-    int max_attempts; /* IPM+polish attempts; tol_mu x1e-3 each retry (default 3) */
+    int max_attempts; /* IPM+polish attempts (default 3); each retry stops the IPM 1e-3 tighter, at most
+                         1e-8 on the second attempt and 1e-12 on the third (1e-4 lower each further one) */
     double tol_mu;    /* IPM stop: mean complementarity, then the polish (default 1e-4) */
     double tol_p;     /* polish primal feasibility, relative to f_max (default 1e-9) */
     double tol_d;     /* polish multiplier sign, relative to gradient scale (default 1e-9) */

@@ -541,7 +541,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             if (++rd >= prm.max_rounds) {
                 keep_tiles = 0;
                 if (++att >= prm.max_attempts) break;
-                tol *= 1e-3;
+                tol = retry_tol(tol, att);
                 it_end += prm.max_iter;
                 mode = PRED;
             }

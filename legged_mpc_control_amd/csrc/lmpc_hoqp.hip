@@ -1075,6 +1075,7 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         // took its crossover answer, the interior point sees those bounds raised to HQ_HFLOOR of the scale -- the
         // margin a level-above iterate would have left -- and the crossover then solves with the true bounds.
         const double hb_true[2] = {W.bd[0], W.bd[1]};
+        const bool raised = any_exact;  // the interior point below sees the raised bounds
         if (any_exact) {
 #pragma unroll
             for (int k = 0; k < 2; ++k)
@@ -1296,12 +1297,25 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             // resume only from a finite iterate that stopped on its criterion (not the cap, not a non-finite direction)
             if (exact || nonfin || numstop || it >= P.max_iter || !(nr > 0 && nd > 0)) break;
         }
+        const bool xo_verified = exact;
         exact = exact || clean;
         // LMPC_QP_CONVERGED: the clean stop, a verified crossover, or -- documented in lmpc_hoqp.h -- the relaxed
         // degenerate stop (complementarity 1e3 below its tolerance, residuals within 1e3 of theirs); a level left on
         // the iteration cap or on a non-finite direction short of that reports LMPC_QP_MAX_ITER
         const bool relaxed = mu_last <= 1e-3 * P.tol_mu * scale && res_last <= 1e3 * P.tol_res * scale;  // final pass
         if (!exact && (it >= P.max_iter || (numstop && !relaxed))) st = 1;
+        // The interior point judged its stop against the raised frozen-row bounds (above).  When this level keeps
+        // its iterate (no verified crossover), the iterate is checked against the TRUE bounds of the higher levels:
+        // a frozen row beyond its true bound by more than the residual tolerance is LMPC_QP_MAX_ITER.
+        if (raised && !xo_verified && st == 0) {
+            double viol = 0.0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = lane + 64 * k;
+                if (r < p) viol = fmax(viol, row_dot<NP>(S, ls, nd, r, S.y) - hb_true[k]);
+            }
+            if (wave_max(viol) > P.tol_res * scale) st = 1;
+        }
         if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16);
         // ---- outputs: w_l = max(0, D_l Z y - g) for the final y, x += Z y ------------------------------
 #pragma unroll

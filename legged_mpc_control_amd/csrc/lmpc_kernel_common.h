@@ -20,7 +20,7 @@ constexpr int LMPC_WAVE = 64;
 #define LMPC_STEP_FRAC 0.99
 #endif
 // Hand-over to the polish: a face is guessed active where z > LMPC_ACT_RATIO * s.  At the hand-over
-// (mean complementarity 1e-6) an active face has z/s ~ z^2/mu >> 1 and an inactive one ~ mu/s^2 << 1; the
+// (mean complementarity tol_mu, default 1e-4) an active face has z/s ~ z^2/mu >> 1 and an inactive one ~ mu/s^2 << 1; the
 // faces in between are near-degenerate, and guessing them active costs fewer polish rounds than guessing
 // them inactive (a wrong active face leaves in the same round a missing one would enter; missing faces
 // enter one per leg-step per round).  numpy replica (tools/polish_guess_proto.py, 1280 config-2 QPs):
@@ -121,6 +121,16 @@ __device__ __forceinline__ double Myaw(double c, double s, int i, int j) {
     if (j == 2) return 0.0;
     if (i == 0) return j == 0 ? c : s;
     return j == 0 ? -s : c;
+}
+
+// Interior-point stop of retry attempt `att` (>= 1) after a polish that did not verify: 1e-3 tighter than the
+// previous attempt's, and never looser than a fixed floor (1e-8 for the second attempt, 1e-12 for the third, 1e-4
+// lower each further one), so the last attempt's iterate is as converged as before the default hand-over moved to
+// 1e-4 (round 3).  Shared by every kernel's retry ladder; lmpc.h (lmpc_options.max_attempts) documents it.
+__device__ __forceinline__ double retry_tol(double tol, int att) {
+    double floor = 1e-8;
+    for (int a = 1; a < att; ++a) floor *= 1e-4;
+    return fmin(tol * 1e-3, floor);
 }
 
 // 1/sqrt(x): hardware estimate + one Newton step (cheaper than the correctly-rounded sqrt + divide).

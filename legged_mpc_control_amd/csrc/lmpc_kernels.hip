@@ -1381,7 +1381,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                     }
                     // retry: tighter interior point, then a fresh polish
                     if (++att >= prm.max_attempts) break;
-                    tol *= 1e-3;
+                    tol = retry_tol(tol, att);
                     it_end += prm.max_iter;
                     mode = PRED;
                 }
