@@ -41,6 +41,8 @@ def parse():
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
                     help="dense-path kernel (lmpc_set_dense_path); default ipm")
+    ap.add_argument("--riccati", choices=["lds", "scratch"], default="lds",
+                    help="Riccati kernel of the QPs no dense kernel takes (lmpc_set_riccati_path); default lds")
     ap.add_argument("--index-offset", type=int, default=0,
                     help="shift the global instance indices (robustness checks on other samples; recorded in config)")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
@@ -67,12 +69,13 @@ def host_cores():
     return usable, {"os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota}
 
 
-def kernel_label(mode):
+def kernel_label(mode, riccati="lds"):
     """The kernels of one solve launch (lmpc_capi.cpp lmpc_solve_batch_device_ex); kernel_ms covers all."""
+    ric = "lmpc_lq_kernel" if riccati == "lds" else "lmpc_qp_kernel"
     if mode == "off":
-        return "lmpc_qp_kernel (Riccati, every QP)"
+        return f"{ric} (Riccati, every QP)"
     dense = "lmpc_gi_kernel" if mode == "gi" else "lmpc_dense_kernel"
-    return f"{dense} (QPs with <= 20 stance leg-steps) + lmpc_qp_kernel (the rest; exits at once when none)"
+    return f"{dense} (QPs with <= 20 stance leg-steps) + {ric} (the rest; exits at once when none)"
 
 
 def global_batch_of(strong, cfg, B, world):
@@ -127,7 +130,7 @@ def main():
     # config 4 13.8 ms against 15.1 ms on the dual active set, profiles/r03/handover/ab_c4_dense.log).  Fixed per
     # context, so no answer depends on it; --dense overrides it.
     dense = args.dense or "ipm"
-    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank, dense_path=dense)
+    solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank, dense_path=dense, riccati_path=args.riccati)
     opts = {}
     for kv in args.opt:
         k, v = kv.split("=", 1)
@@ -294,6 +297,8 @@ def main():
     # (configs 3 and 5 run the Riccati kernel by default: H > 16 has no dense path)
     overridden = args.dense is not None and args.dense != "ipm"
     wl = (f"{wl_name}/{mode}" if overridden else wl_name) if args.batch is None else None
+    if wl is not None and args.riccati != "lds":
+        wl += "/scratch"
     try:
         tr = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
         if wl in tr:
@@ -344,14 +349,21 @@ def main():
             },
             "roofline": {
                 # fp64 compute, not HBM; the counters show fp64 VALU work issued by a latency-bound wave (one
-                # QP per SIMD), not matrix-core throughput; the fp64 peak is the same for both
+                # QP per SIMD), not matrix-core throughput; the fp64 peak is the same for both.
+                # achieved / frac: the fp64 flops the kernels really execute (calibrated SQ counters of this workload,
+                # profiles/pmc_flops.json) when committed for it, else the contract figure; frac_contract is always
+                # SURVEY.md 8(d)'s contract flops (which price a dense N = 12H condensation the Riccati kernels never
+                # execute: ~3x the executed flops at H = 30) -- VERDICT r3 item 3
                 "bound": "fp64-valu-latency",
-                "achieved": achieved_tf,
+                "achieved": executed["achieved"] if executed else achieved_tf,
                 "peak": roofline.FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": achieved_tf / roofline.FP64_PEAK_TFLOPS,
+                "frac": executed["frac"] if executed else achieved_tf / roofline.FP64_PEAK_TFLOPS,
+                "frac_source": "executed (PMC)" if executed else "contract (SURVEY 8d)",
+                "frac_contract": achieved_tf / roofline.FP64_PEAK_TFLOPS,
+                "achieved_contract": achieved_tf,
                 "traffic": traffic_bytes,
-                "kernel": kernel_label(mode),
+                "kernel": kernel_label(mode, args.riccati),
                 "kernel_ms": kernel_ms,
                 "flop_per_qp": flop_per_qp,
                 "flop_model": flop_model,
@@ -373,6 +385,7 @@ def main():
             },
             "qp_status": {"converged": int(stats[0]), "max_iter": int(stats[1]), "nan": int(stats[2])},
             "dense_path": mode,
+            "riccati_path": args.riccati,
             "ipm_iters_mean": ipm_mean,
             "polish_rounds_mean": pol_mean,
             "ipm_iters_max": int(np.max(it & 0xFFFF)),

@@ -49,9 +49,10 @@
 extern "C" {
 #endif
 
-#define LMPC_ABI_VERSION 5 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
+#define LMPC_ABI_VERSION 6 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
                               4: warm start (lmpc_solve_batch_warm, lmpc_shift_active_set);
-                              5: dense-path caps in lmpc_options, no environment overrides */
+                              5: dense-path caps in lmpc_options, no environment overrides;
+                              6: Riccati-kernel selection (lmpc_set_riccati_path) */
 #define LMPC_MAX_HORIZON 32
 
 /* return codes (API level) */
@@ -140,6 +141,16 @@ int lmpc_set_params(lmpc_ctx* ctx, const lmpc_params* p);
 #define LMPC_DENSE_GI 2
 int lmpc_set_dense_path(lmpc_ctx* ctx, int path);
 int lmpc_get_dense_path(const lmpc_ctx* ctx);
+
+/* Riccati path (ABI 6).  The QPs no dense kernel takes (more than 20 stance leg-steps, H > 16, or a dense QP
+ * left without a verified optimum) run on LMPC_RICCATI_LDS (default since round 4: every per-stage factor in
+ * LDS, no global workspace) or LMPC_RICCATI_SCRATCH (the round-1..3 kernel: factors in a per-QP global
+ * workspace).  Both return the same verified optimum.  Warm-started solves (lmpc_solve_batch_warm) always run
+ * on LMPC_RICCATI_SCRATCH.  Fixed per context, never per launch. */
+#define LMPC_RICCATI_SCRATCH 0
+#define LMPC_RICCATI_LDS 1
+int lmpc_set_riccati_path(lmpc_ctx* ctx, int path);
+int lmpc_get_riccati_path(const lmpc_ctx* ctx);
 
 /* Pre-allocates the per-QP factor workspace for batches up to `batch` (the
  * device path grows it on demand; call this before capturing a HIP graph). */

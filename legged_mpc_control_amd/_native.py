@@ -34,9 +34,9 @@ EXPORTED_SYMBOLS = (
     # GRF -> joint torque
     "lmpc_leg_kin_default", "lmpc_foot_jacobian", "lmpc_grf_to_torque", "lmpc_grf_to_torque_device",
     # ABI 3: dense-path selection
-    "lmpc_set_dense_path", "lmpc_get_dense_path",
+    "lmpc_set_dense_path", "lmpc_get_dense_path", "lmpc_set_riccati_path", "lmpc_get_riccati_path",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
 # include/lmpc/lmpc_hoqp.h: batched hierarchical QP (whole-body control)
 HOQP_SYMBOLS = (
     "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
@@ -194,6 +194,10 @@ def lib():
         L.lmpc_set_dense_path.restype = ctypes.c_int
         L.lmpc_get_dense_path.argtypes = [vp]
         L.lmpc_get_dense_path.restype = ctypes.c_int
+        L.lmpc_set_riccati_path.argtypes = [vp, ctypes.c_int]
+        L.lmpc_set_riccati_path.restype = ctypes.c_int
+        L.lmpc_get_riccati_path.argtypes = [vp]
+        L.lmpc_get_riccati_path.restype = ctypes.c_int
         L.lmpc_reserve.argtypes = [vp, ctypes.c_int]
         L.lmpc_reserve.restype = ctypes.c_int
         L.lmpc_solve_batch.argtypes = [vp, dp, u8p, ctypes.c_int, dp, i32p, i32p]

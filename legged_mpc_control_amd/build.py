@@ -24,11 +24,12 @@ HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 SCHED_FLAGS = {
     "lmpc_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "lmpc_dense.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "lmpc_lq.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "lmpc_gi.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
     "lmpc_hoqp.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
 
-SOURCES = ["lmpc_kernels.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
+SOURCES = ["lmpc_kernels.hip", "lmpc_lq.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
            "hoqp_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
 HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_hoqp_device.h"]
 

@@ -18,6 +18,8 @@ namespace lmpc {
 hipError_t launch_qp(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                      int batch, double* grf, int32_t* status, int32_t* iters, double* scratch, const uint8_t* done,
                      hipStream_t stream);
+hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals, int batch,
+                     double* grf, int32_t* status, int32_t* iters, const uint8_t* done, hipStream_t stream);
 hipError_t launch_gi(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                      int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
 hipError_t launch_dense(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
@@ -45,7 +47,8 @@ struct lmpc_ctx {
     uint8_t* d_out = nullptr;
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
-    double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2), grown on demand
+    int riccati = LMPC_RICCATI_SCRATCH;  // the Riccati kernel of cold solves (lmpc_set_riccati_path)
+    double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2) of the scratch kernel, grown on demand
     uint8_t* d_done = nullptr;    // per-QP flag: solved by the dense-path kernel (else the Riccati kernel solves it)
     size_t scratch_qps = 0;
     double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
@@ -161,6 +164,16 @@ void free_bufs(lmpc_ctx* c) {
     c->d_in = c->d_out = c->h_in = c->h_out = nullptr;
 }
 
+// The Riccati kernel of a cold solve: the LDS-resident one (lmpc_lq.hip) or the scratch one (lmpc_kernels.hip,
+// which needs the per-QP global workspace, grown by lmpc_reserve).
+hipError_t launch_riccati(const lmpc_ctx* c, const lmpc::DevParams& prm, const double* rec, const uint8_t* con,
+                          const double* nrm, int batch, double* grf, int32_t* st, int32_t* it, const uint8_t* done,
+                          hipStream_t s) {
+    if (c->riccati == LMPC_RICCATI_LDS && !prm.warm_act && !prm.act_out)
+        return lmpc::launch_lq(prm, rec, con, nrm, batch, grf, st, it, done, s);
+    return lmpc::launch_qp(prm, rec, con, nrm, batch, grf, st, it, c->d_scratch, done, s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -256,6 +269,14 @@ int lmpc_set_dense_path(lmpc_ctx* c, int path) {
 
 int lmpc_get_dense_path(const lmpc_ctx* c) { return c ? c->prm.dense : LMPC_ERR_ARG; }
 
+int lmpc_set_riccati_path(lmpc_ctx* c, int path) {
+    if (!c || (path != LMPC_RICCATI_SCRATCH && path != LMPC_RICCATI_LDS)) return LMPC_ERR_ARG;
+    c->riccati = path;
+    return LMPC_OK;
+}
+
+int lmpc_get_riccati_path(const lmpc_ctx* c) { return c ? c->riccati : LMPC_ERR_ARG; }
+
 int lmpc_reserve(lmpc_ctx* c, int batch) {
     if (!c || batch < 0) return LMPC_ERR_ARG;
     if ((size_t)batch <= c->scratch_qps) return LMPC_OK;
@@ -301,8 +322,8 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
     else if (e == hipSuccess && c->prm.dense == 1)
         e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
     if (e == hipSuccess)
-        e = lmpc::launch_qp(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_scratch,
-                            c->prm.dense ? c->d_done : nullptr, s);
+        e = launch_riccati(c, c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters,
+                           c->prm.dense ? c->d_done : nullptr, s);
     if (e == hipSuccess) e = ctx_leave(c, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;
@@ -375,8 +396,7 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
         e = gi ? lmpc::launch_gi(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s)
                : lmpc::launch_dense(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s);
     if (e == hipSuccess && n_ric)
-        e = lmpc::launch_qp(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch,
-                            prm.dense ? d_done : nullptr, s);
+        e = launch_riccati(c, prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, prm.dense ? d_done : nullptr, s);
     if (e == hipSuccess) e = ctx_leave(c, s);
     if (e != hipSuccess) return launch_rc(e);
     // one copy back: [grf | status | iters], plus the hand-over flags (dense path) or the active set (warm)
@@ -392,7 +412,7 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
         for (int b = 0; b < batch && !left; ++b) left = hd[b] == 0;
         if (left) {
             if ((size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
-            e = lmpc::launch_qp(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, c->d_scratch, d_done, s);
+            e = launch_riccati(c, prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s);
             if (e == hipSuccess) e = ctx_leave(c, s);
             if (e != hipSuccess) return launch_rc(e);
             if (hipMemcpyAsync(c->h_out, c->d_out, ngrf + 2 * nst, hipMemcpyDeviceToHost, s) != hipSuccess ||

@@ -1,0 +1,1068 @@
+// lmpc_lq.hip -- the Riccati path with every per-stage factor in LDS (gfx950), round 4.
+//
+// One 64-lane wavefront per QP, no global scratch and no outlined calls: the per-stage factors the vector passes
+// need are kept in a 207-double LDS slot per stage (19.7 KB per QP at H = 10, so 8 QPs -- two waves per SIMD --
+// share a CU), and everything else lives in registers.  The QP, the interior point and the polish are those of
+// lmpc_kernels.hip (ConvexQPSolver.cpp:16-346 restated); what changes is how the Newton systems are
+// solved (numpy replica step for step: tools/lq_proto.py):
+//
+//   factorisation (stage k = H-1 .. 0), value function of the augmented state [x; 1] in one 16x16 MFMA tile
+//   (P^ = [P p; p' c]: its column 12 is the linear term p, so the backward vector pass of the right-hand side the
+//   factorisation is given comes for free):
+//       C   = P^ B^,  B^ rows 6-11 = [Bt | dv]            -> v = P d (column 12)
+//       Guu = Bt' P22 Bt, + Rr_j at each 3x3 leg pivot (Rr is block diagonal: it enters only its own pivot block)
+//       block Cholesky by legs with L^-1 and X = L^-1 [0 | Bt' | rr] eliminated alongside (as lmpc_kernels.hip)
+//       KH  = X'X                                          -> K = V'V (rows/cols 6-11), rho = Bt Guu^-1 rr (col 12)
+//       S   = X'L^-1 (rows 6-11) = Bt Guu^-1              (interior point only: the corrector's rho = S rr')
+//       PA  = P^ A^,  A^ = [A d; 0 1]                       -> Z = rows 6-11 of PA (6 x 13; column 12 = za = v2 + p2)
+//       P^_k = Q^_k + A^'PA - M'KH M'  (M' = PA with row 12 = e12), Q^_k column 12 = -Q x_ref,k-1
+//   stored per stage: Z (78), K (21, packed), rho (6), S (72), v (12), x (12), dv (6)
+//   forward sweep      w = Z x + za ;  x' = A x + d - [0; K w + rho]
+//   inputs (parallel)  from the costate lambda2 = Z A^-1 x' + za - v2 (= P2 x' + p2): u_j = -Rr_j^-1 (rr_j + Bt_j' lambda2)
+//                      (lane-local 3x3 solves: Rr is the leg-step's own input Hessian block)
+//   corrector          rho = S rr' (parallel), then the backward sweep p_k = q_k + A'y - Z'(K za + rho), y = p + v,
+//                      za = y[6:12], then the forward sweep and the inputs as above
+//   polish check       the adjoint lambda from the trajectory (independent of the factorisation), as lmpc_kernels.hip
+//
+// The stage-k operands of the factorisation come from LDS (Bt in the S slot, rr in the x slot, dv, written by the
+// leg-step lanes before it) and from the leg-step lanes' registers (Rr_j, by readlane: wave-uniform per stage and leg),
+// fetched one stage ahead.  QPs the condensed dense kernel solved are skipped (its hand-over flags).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "lmpc/lmpc.h"
+#include "lmpc_device.h"
+#include "lmpc_kernel_common.h"
+
+namespace lmpc {
+
+#ifdef LMPC_STAMPS
+constexpr int LQ_STAMP_QPS = 4096;
+constexpr int LQ_STAMP_N = 12;
+__device__ unsigned long long lmpc_lq_stamps[LQ_STAMP_QPS][LQ_STAMP_N];
+#define LQ_STAMP_DECL unsigned long long _lq_acc[LQ_STAMP_N] = {}; unsigned long long _lq_t0 = __builtin_readcyclecounter();
+#define LQ_STAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _lq_acc[i] += _t - _lq_t0; _lq_t0 = _t; } while (0)
+#define LQ_STAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < LQ_STAMP_QPS) for (int _i = 0; _i < LQ_STAMP_N; ++_i) lmpc_lq_stamps[qp][_i] = _lq_acc[_i]; } while (0)
+#else
+#define LQ_STAMP_DECL
+#define LQ_STAMP(i) do {} while (0)
+#define LQ_STAMP_FLUSH(qp) do {} while (0)
+#endif
+
+#ifdef LMPC_LQ_DEBUG
+__device__ double lmpc_lq_dbg[8192];
+__device__ double lmpc_lq_dbg_u[384];
+__device__ double lmpc_lq_dbg2[8192];
+extern "C" int lmpc_debug_lq_dump(double* lds, double* u, double* lds2) {
+    return (hipMemcpyFromSymbol(lds, HIP_SYMBOL(lmpc_lq_dbg), sizeof(double) * 8192) == hipSuccess &&
+            hipMemcpyFromSymbol(lds2, HIP_SYMBOL(lmpc_lq_dbg2), sizeof(double) * 8192) == hipSuccess &&
+            hipMemcpyFromSymbol(u, HIP_SYMBOL(lmpc_lq_dbg_u), sizeof(double) * 384) == hipSuccess) ? 0 : -1;
+}
+#endif
+
+// ---- LDS layout (doubles) ----------------------------------------------------------------------------------
+// per-stage slot
+constexpr int LQ_Z = 0;      // 78: Z = rows 6-11 of P^_{k+1} A^_k, 6 x 13 row-major (column 12: za = v2 + p2)
+constexpr int LQ_K = 78;     // 21: K = Bt Guu^-1 Bt', packed lower (pk6)
+constexpr int LQ_RHO = 99;   // 6:  rho = Bt Guu^-1 rr; after the forward sweep lambda2 (inputs / adjoint)
+constexpr int LQ_S = 105;    // 72: S = Bt Guu^-1 (6 x 12); before the factorisation Bt = G0 T (6 x 12)
+constexpr int LQ_V = 177;    // 12: v = P_{k+1} d_k
+constexpr int LQ_X = 189;    // 12: x_{k+1}; before the factorisation rr (the input linear term, 12)
+constexpr int LQ_DV = 201;   // 6:  d_k[6:12] = G0 up - g dt e5
+constexpr int LQ_SLOT = 207;
+// fixed part
+constexpr int LQF_HDR = 0;     // 40: x0(12) R(9) feet(12)
+constexpr int LQF_G0 = 40;     // 72: B rows 6-11 (terrain: G0 blkdiag(R_j))
+constexpr int LQF_QW = 112;    // 12: state weights
+constexpr int LQF_ZERO = 124;  // 4:  always 0
+constexpr int LQF_TF = 128;    // 36: terrain frames R_j (row-major)
+constexpr int LQF_RB = 164;    // 24: terrain R_j' diag(r_j) R_j packed [xx xy xz yy yz zz]
+constexpr int LQF_PV = 188;    // 144: pivot rows of Guu, L^-1, X (48 each)
+constexpr int LQF_SINK = 332;  // 64: stores of lanes that hold no pivot row / no output
+constexpr int LQF_EX = 396;    // 32: exchange buffer of the serial sweeps
+constexpr int LQF_CS = 428;    // 2H: cos / sin of the reference yaw per step
+constexpr int LQF_FIXED = 428;
+__host__ __device__ constexpr int lq_lds_doubles(int H) { return LQF_FIXED + 2 * H + LQ_SLOT * H; }
+size_t lq_lds_bytes(int H) { return (size_t)lq_lds_doubles(H) * sizeof(double); }
+
+__device__ __forceinline__ constexpr int pk6(int a, int b) {  // packed lower 6x6, any order
+    return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a;
+}
+
+// entries of dt N(yaw) = A_k - I (rows 0-5, columns 6-11)
+__device__ __forceinline__ double lq_dtN(int r, int c, double ck, double sk, double dt) {
+    if (r >= 12 || c >= 12) return 0.0;
+    double v = 0.0;
+    if (r < 3 && c >= 6 && c < 9) {
+        const int j = c - 6;
+        const double m = (r == 0) ? ((j == 0) ? ck : (j == 1) ? sk : 0.0)
+                       : (r == 1) ? ((j == 0) ? -sk : (j == 1) ? ck : 0.0)
+                                  : ((j == 2) ? 1.0 : 0.0);
+        v += dt * m;
+    }
+    if (r >= 3 && r < 6 && c == r + 6) v += dt;
+    return v;
+}
+
+// (A x)[r], (A^-1 x)[r] (A = I + dt N, N nilpotent: A^-1 = I - dt N), (A' w)[r]
+template <class Ptr>
+__device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, double dt, double sgn) {
+    if (r == 0) return x[0] + sgn * dt * (ck * x[6] + sk * x[7]);
+    if (r == 1) return x[1] + sgn * dt * (-sk * x[6] + ck * x[7]);
+    if (r == 2) return x[2] + sgn * dt * x[8];
+    if (r < 6) return x[r] + sgn * dt * x[r + 6];
+    return x[r];
+}
+template <class Ptr>
+__device__ __forceinline__ double lq_Atw(Ptr w, int r, double ck, double sk, double dt) {
+    if (r == 6) return w[6] + dt * (ck * w[0] - sk * w[1]);
+    if (r == 7) return w[7] + dt * (sk * w[0] + ck * w[1]);
+    if (r == 8) return w[8] + dt * w[2];
+    if (r >= 9) return w[r] + dt * w[r - 6];
+    return w[r];
+}
+
+__device__ __forceinline__ int lq_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// lane-local solve of the symmetric positive definite 3x3 system R y = b (R packed [xx xy xz yy yz zz])
+__device__ __forceinline__ void sym3_solve(const double R[6], const double b[3], double y[3]) {
+    const double i00 = rsq_nr(R[0]);
+    const double l10 = R[1] * i00, l20 = R[2] * i00;
+    const double i11 = rsq_nr(fma(-l10, l10, R[3]));
+    const double l21 = fma(-l20, l10, R[4]) * i11;
+    const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, R[5])));
+    const double c0 = b[0] * i00;
+    const double c1 = fma(-l10, c0, b[1]) * i11;
+    const double c2 = fma(-l21, c1, fma(-l20, c0, b[2])) * i22;
+    y[2] = c2 * i22;
+    y[1] = fma(-l21, y[2], c1) * i11;
+    y[0] = fma(-l20, y[2], fma(-l10, y[1], c0)) * i00;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// The kernel.  LS = leg-steps per lane (ceil(4H/64)); TERRAIN: per-leg contact frames (lmpc_kernels.hip).
+// Two waves per SIMD at LS = 1 (256 registers), one at LS = 2.
+// ---------------------------------------------------------------------------------------------------------
+template <int LS, bool TERRAIN>
+__global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevParams prm, const double* __restrict__ rec,
+                                                                     const uint8_t* __restrict__ contact,
+                                                                     const double* __restrict__ normals, int batch,
+                                                                     double* __restrict__ grf, int32_t* __restrict__ status,
+                                                                     int32_t* __restrict__ iters,
+                                                                     const uint8_t* __restrict__ dense_done) {
+    extern __shared__ __attribute__((aligned(16))) double lq_smem[];
+    const int qp = blockIdx.x;
+    if (qp >= batch) return;
+    const int lane = threadIdx.x;
+    const int H = prm.H;
+    if (prm.dense) {  // QPs with 1..DENSE_MAX_LS stance leg-steps went to a dense-path kernel (H <= 16 here)
+        const bool stl = lane < 4 * H && contact[(size_t)qp * 4 * H + lane] != 0;
+        const int n = __popcll(__ballot(stl));
+        if (n >= 1 && n <= DENSE_MAX_LS && (!dense_done || dense_done[qp])) return;
+    }
+    ldouble* const sm = (ldouble*)lq_smem;
+    ldouble* const hdr = sm + LQF_HDR;
+    ldouble* const G0s = sm + LQF_G0;
+    ldouble* const qw = sm + LQF_QW;
+    ldouble* const zero = sm + LQF_ZERO;
+    ldouble* const tf = sm + LQF_TF;
+    ldouble* const rbt = sm + LQF_RB;
+    ldouble* const pv = sm + LQF_PV;
+    ldouble* const sink = sm + LQF_SINK;
+    ldouble* const ex = sm + LQF_EX;
+    ldouble* const cs = sm + LQF_CS;
+    ldouble* const slots = sm + LQF_FIXED + 2 * H;
+    const int RL = 33 + 12 * H;
+    const double* rin = rec + (size_t)qp * RL;
+    const double* xr = rin + 33;  // x_ref (global, L2-resident after its first use)
+    const double mu = prm.mu, fzmax = prm.fmax, dt = prm.dt;
+    LQ_STAMP_DECL
+
+    // ---- prologue: record, terrain frames, I_w^-1, G0, yaw cos / sin ----------------------------------------
+    if (lane < 33) hdr[lane] = rin[lane];
+    if (lane < 12) qw[lane] = prm.q[lane];
+    if (lane < 4) zero[lane] = 0.0;
+    if constexpr (TERRAIN) {
+        if (lane < 4) {
+            const double* nin = normals + (size_t)qp * 12 + 3 * lane;
+            const double n0 = nin[0], n1 = nin[1], n2 = nin[2];
+            const double nn = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+            const double nx = n0 / nn, ny = n1 / nn, c = n2 / nn;
+            const double h = 1.0 / (1.0 + c);
+            const double R[9] = {1.0 - nx * nx * h, -nx * ny * h, nx, -nx * ny * h, 1.0 - ny * ny * h, ny, -nx, -ny, c};
+#pragma unroll
+            for (int e = 0; e < 9; ++e) tf[9 * lane + e] = R[e];
+            const double r0 = prm.r[3 * lane], r1 = prm.r[3 * lane + 1], r2 = prm.r[3 * lane + 2];
+            int e = 0;
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = a; b < 3; ++b) rbt[6 * lane + e++] = r0 * R[a] * R[b] + r1 * R[3 + a] * R[3 + b] + r2 * R[6 + a] * R[6 + b];
+        }
+    }
+    for (int k = lane; k < H; k += 64) {
+        double sn, cn;
+        sincos(xr[12 * k + 2], &sn, &cn);
+        cs[2 * k] = cn;
+        cs[2 * k + 1] = sn;
+    }
+    LMPC_SYNC();
+    {
+        double iw[9];
+        const ldouble* R = hdr + LMPC_REC_ROT;
+        double RI[9], Iw[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                RI[i * 3 + j] = R[i * 3 + 0] * prm.Ib[0 * 3 + j] + R[i * 3 + 1] * prm.Ib[1 * 3 + j] + R[i * 3 + 2] * prm.Ib[2 * 3 + j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                Iw[i * 3 + j] = RI[i * 3 + 0] * R[j * 3 + 0] + RI[i * 3 + 1] * R[j * 3 + 1] + RI[i * 3 + 2] * R[j * 3 + 2];
+        const double c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
+        const double c01 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
+        const double c02 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
+        const double id = 1.0 / (Iw[0] * c00 + Iw[1] * c01 + Iw[2] * c02);
+        iw[0] = c00 * id;
+        iw[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * id;
+        iw[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * id;
+        iw[3] = c01 * id;
+        iw[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * id;
+        iw[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * id;
+        iw[6] = c02 * id;
+        iw[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * id;
+        iw[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * id;
+        // G0 = dt [I_w^-1 skew(r_j) ; I/m] (ConvexQPSolver.cpp:198-212; Utils.cpp:89-95), terrain: G0 blkdiag(R_j)
+        for (int e = lane; e < 72; e += 64) {
+            const int r = e / 12, c = e % 12, j = c / 3, cc = c % 3;
+            double w[3];
+            if (r < 3) {
+                const ldouble* ft = hdr + LMPC_REC_FEET + 3 * j;
+                // row r of I_w^-1 by selects (a dynamically indexed private array would live in scratch memory)
+                const double a0 = r == 0 ? iw[0] : r == 1 ? iw[3] : iw[6];
+                const double a1 = r == 0 ? iw[1] : r == 1 ? iw[4] : iw[7];
+                const double a2 = r == 0 ? iw[2] : r == 1 ? iw[5] : iw[8];
+                w[0] = dt * (a1 * ft[2] - a2 * ft[1]);
+                w[1] = dt * (-a0 * ft[2] + a2 * ft[0]);
+                w[2] = dt * (a0 * ft[1] - a1 * ft[0]);
+            } else {
+                w[0] = w[1] = w[2] = 0.0;
+                w[r - 3] = dt / prm.mass;
+            }
+            double v = w[cc];
+            if constexpr (TERRAIN) {
+                const ldouble* Rj = tf + 9 * j;
+                v = w[0] * Rj[cc] + w[1] * Rj[3 + cc] + w[2] * Rj[6 + cc];
+            }
+            G0s[e] = v;
+        }
+    }
+    LMPC_SYNC();
+
+    // ---- leg-step ownership, starting point (lmpc_kernels.hip) -----------------------------------------------
+    bool st[LS], valid[LS];
+    int lsk[LS], lsj[LS];
+    double f[LS][3], s[LS][5], z[LS][5];
+    // long-lived per leg-step: the iterate (f, s, z), the stage data of the current Newton system (Rr: input
+    // Hessian block, rr: linear term), the last solution u and the predictor's ua.  The polish's null-space
+    // basis (T, up) is recomputed where it is needed (leg_basis), so it holds no registers across the solves.
+    double Rr[LS][6], rr[LS][3], u[LS][3], ua[LS][3];
+    int nst_loc = 0;
+#pragma unroll
+    for (int t = 0; t < LS; ++t) {
+        const int ls = lane + 64 * t;
+        valid[t] = ls < 4 * H;
+        lsk[t] = valid[t] ? (ls >> 2) : 0;
+        lsj[t] = ls & 3;
+        st[t] = valid[t] && contact[(size_t)qp * 4 * H + ls] != 0;
+        nst_loc += st[t] ? 1 : 0;
+        f[t][0] = f[t][1] = 0.0;
+        const double cnt = quad_sum(st[t] ? 1.0 : 0.0);
+        f[t][2] = st[t] ? fmin(0.5 * fzmax, prm.mass * prm.grav / fmax(cnt, 1.0)) : 0.0;
+        double o[5];
+        cons_resid(f[t], mu, fzmax, o);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            s[t][i] = st[t] ? -o[i] : 1.0;
+            z[t][i] = 1.0 / s[t][i];
+        }
+#pragma unroll
+        for (int m = 0; m < 3; ++m) u[t][m] = ua[t][m] = rr[t][m] = 0.0;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) Rr[t][e] = (e == 0 || e == 3 || e == 5) ? 1.0 : 0.0;
+    }
+    const double nst = wave_sum((double)nst_loc);
+    LQ_STAMP(0);  // prologue
+
+    const int lc = lane & 15, lr = lane >> 4;  // accumulator layout: column lc, rows lr + 4i
+
+    // ---- the interior point / polish state machine -----------------------------------------------------------
+    int qstatus = LMPC_QP_CONVERGED, ipm_it = 0, prounds = 0;
+    bool done = false;
+    if (nst > 0.5) {
+        enum { PRED = 0, CORR = 1, POLISH = 2 };
+        const double mc = 5.0 * nst;
+        double tol = prm.tol_mu;
+        int att = 0, rd = 0, it_end = prm.max_iter, mode = PRED;
+        int act[LS];
+        bool apex[LS];
+#pragma unroll
+        for (int t = 0; t < LS; ++t) {
+            act[t] = 0;
+            apex[t] = false;
+        }
+        double mu_c = 0.0, smu = 0.0;
+        for (;;) {
+            // ======== leg-step work: stage data of the Newton system ========
+            if (mode == PRED) {
+                double loc = 0.0;
+#pragma unroll
+                for (int t = 0; t < LS; ++t)
+                    if (st[t])
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) loc += s[t][i] * z[t][i];
+                mu_c = wave_sum(loc) / mc;
+                if (mu_c < tol || ipm_it >= it_end) {
+                    // active set from the interior point: z > LMPC_ACT_RATIO s, lift-off legs -> apex
+#pragma unroll
+                    for (int t = 0; t < LS; ++t) {
+                        act[t] = 0;
+                        if (!st[t]) continue;
+#pragma unroll
+                        for (int i = 0; i < 5; ++i)
+                            if (z[t][i] > LMPC_ACT_RATIO * s[t][i]) act[t] |= 1 << i;
+                        const double fm = fmax(fabs(f[t][0]), fmax(fabs(f[t][1]), fabs(f[t][2])));
+                        if (fm < 1e-6 * fzmax) act[t] = 15;
+                    }
+                    mode = POLISH;
+                    rd = 0;
+                }
+            }
+            // stage data per leg-step: Rr (the input Hessian block), rr (linear term), and for the factorisation
+            // Bt = G0_j T -> S slot, rr -> x slot, G0_j up (-> dv) with T the leg's null-space basis (I for a stance leg
+            // in the interior point, 0 for a swing leg) and up its particular solution (polish only)
+            double du[LS][6];
+            bool cpl[LS];
+#pragma unroll
+            for (int t = 0; t < LS; ++t) {
+                const int j = lsj[t];
+                double rb[6];
+                if constexpr (TERRAIN) {
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) rb[e] = rbt[6 * j + e];
+                } else {
+                    rb[0] = prm.r[3 * j]; rb[1] = 0.0; rb[2] = 0.0;
+                    rb[3] = prm.r[3 * j + 1]; rb[4] = 0.0; rb[5] = prm.r[3 * j + 2];
+                }
+                double T[9], up[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+                for (int e = 0; e < 9; ++e) T[e] = (e % 4 == 0 && st[t]) ? 1.0 : 0.0;
+                if (mode == POLISH) {
+                    apex[t] = false;
+                    if (st[t]) apex[t] = leg_basis(act[t], mu, fzmax, T, up);
+                    // Rr = T' Rb T (fixed components -> identity), rr = T' Rb up
+                    const double R3[9] = {rb[0], rb[1], rb[2], rb[1], rb[3], rb[4], rb[2], rb[4], rb[5]};
+                    bool fixed[3];
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) fixed[a] = T[a] == 0.0 && T[3 + a] == 0.0 && T[6 + a] == 0.0;
+                    double RT[9], Ru[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                        for (int b = 0; b < 3; ++b) RT[q * 3 + b] = R3[q * 3 + 0] * T[0 * 3 + b] + R3[q * 3 + 1] * T[1 * 3 + b] + R3[q * 3 + 2] * T[2 * 3 + b];
+                        Ru[q] = R3[q * 3 + 0] * up[0] + R3[q * 3 + 1] * up[1] + R3[q * 3 + 2] * up[2];
+                    }
+                    int e = 0;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                        for (int b = a; b < 3; ++b) {
+                            double v = T[0 * 3 + a] * RT[0 * 3 + b] + T[1 * 3 + a] * RT[1 * 3 + b] + T[2 * 3 + a] * RT[2 * 3 + b];
+                            if (fixed[a] || fixed[b]) v = (a == b) ? 1.0 : 0.0;
+                            Rr[t][e++] = v;
+                        }
+                        rr[t][a] = fixed[a] ? 0.0 : T[0 * 3 + a] * Ru[0] + T[1 * 3 + a] * Ru[1] + T[2 * 3 + a] * Ru[2];
+                    }
+                } else if (mode == PRED) {
+                    // interior point: Rr = Rb + C'WC, rr = C'W(s - b) (predictor); identity / zero on swing legs
+                    double W[5] = {0, 0, 0, 0, 0}, wv[5] = {0, 0, 0, 0, 0};
+                    if (st[t]) {
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) {
+                            W[i] = z[t][i] * rcp_nr(s[t][i]);
+                            wv[i] = W[i] * (s[t][i] - (i == 4 ? fzmax : 0.0));
+                        }
+                    }
+                    const double sx = W[0] + W[1], sy = W[2] + W[3];
+                    Rr[t][0] = st[t] ? rb[0] + sx : 1.0;
+                    Rr[t][1] = st[t] ? rb[1] : 0.0;
+                    Rr[t][2] = st[t] ? rb[2] + mu * (W[0] - W[1]) : 0.0;
+                    Rr[t][3] = st[t] ? rb[3] + sy : 1.0;
+                    Rr[t][4] = st[t] ? rb[4] + mu * (W[2] - W[3]) : 0.0;
+                    Rr[t][5] = st[t] ? rb[5] + mu * mu * (sx + sy) + W[4] : 1.0;
+                    cons_tw(wv, mu, rr[t]);
+                }
+                // (CORR: Rr unchanged; rr was set to the corrector's by the predictor step below)
+                bool cp = false;
+#pragma unroll
+                for (int e = 0; e < 9; ++e) cp |= T[e] != 0.0;
+                cpl[t] = valid[t] && cp;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) du[t][m] = 0.0;
+                if (mode != CORR && valid[t]) {
+                    ldouble* sl = slots + lsk[t] * LQ_SLOT;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) {
+                        const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) sl[LQ_S + m * 12 + 3 * j + a] = g0 * T[0 * 3 + a] + g1 * T[1 * 3 + a] + g2 * T[2 * 3 + a];
+                        du[t][m] = g0 * up[0] + g1 * up[1] + g2 * up[2];
+                    }
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) sl[LQ_X + 3 * j + a] = rr[t][a];
+                }
+            }
+            // dv_k = sum over the stage's legs of G0_j up - g dt e5 (lanes 4k..4k+3 of a stage: a quad)
+            if (mode != CORR) {
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) du[t][m] = quad_sum(du[t][m]);
+                    if (valid[t] && lsj[t] == 0) {
+                        ldouble* sl = slots + lsk[t] * LQ_SLOT;
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) sl[LQ_DV + m] = du[t][m] - (m == 5 ? prm.grav * dt : 0.0);
+                    }
+                }
+            }
+            // coupled legs per stage (T != 0): ballot, one word per leg-step slot
+            unsigned long long cmask[LS];
+#pragma unroll
+            for (int t = 0; t < LS; ++t) cmask[t] = __ballot(cpl[t]);
+            LMPC_SYNC();
+            LQ_STAMP(1);  // leg-step work
+
+            if (mode == CORR) {
+                // ======== corrector: rho = S rr' (per stage, quad-reduced), then the backward sweep ========
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    double pr[6];
+                    const int j = lsj[t];
+                    const ldouble* sl = slots + lsk[t] * LQ_SLOT;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m)
+                        pr[m] = sl[LQ_S + m * 12 + 3 * j] * rr[t][0] + sl[LQ_S + m * 12 + 3 * j + 1] * rr[t][1] +
+                                sl[LQ_S + m * 12 + 3 * j + 2] * rr[t][2];
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) pr[m] = quad_sum(pr[m]);
+                    if (valid[t] && j == 0) {
+                        ldouble* so_ = slots + lsk[t] * LQ_SLOT;
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) so_[LQ_RHO + m] = pr[m];
+                    }
+                }
+                LMPC_SYNC();
+                // backward: y = p_{k+1} + v_k, za = y[6:12] -> Z column 12, t = K za + rho, p_k = q_k + A'y - Z't.
+                // Lanes 0-11 hold p (lane r <-> p[r]); y goes through the exchange buffer, t by readlane.
+                {
+                    const int r = lane < 12 ? lane : 0;
+                    double p = lane < 12 ? -qw[r] * xr[(H - 1) * 12 + r] : 0.0;
+                    for (int k = H - 1; k >= 0; --k) {
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        const double y = p + sl[LQ_V + r];
+                        if (lane < 12) ex[r] = y;
+                        if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
+                        LMPC_SYNC();
+                        if (k == 0) break;
+                        // t_m = sum_n K[m][n] y[6+n] + rho_m, lanes 0-5
+                        const int m = lane < 6 ? lane : 0;
+                        double tv = sl[LQ_RHO + m];
+#pragma unroll
+                        for (int n = 0; n < 6; ++n) tv = fma(sl[LQ_K + pk6(m, n)], ex[6 + n], tv);
+                        const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                        double pn = -qw[r] * xr[(k - 1) * 12 + r] + lq_Atw(ex, r, ck, sk, dt);
+#pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) pn = fma(-sl[LQ_Z + mm * 13 + r], readlane_f64(tv, mm), pn);
+                        p = pn;
+                        LMPC_SYNC();
+                    }
+                }
+                LQ_STAMP(2);  // corrector backward
+            } else {
+                // ======== factorisation with the fused backward pass (stage k = H-1 .. 0) ========
+                // The lane-static operand maps are recomputed in every stage from an opaque copy of the lane index
+                // (integer work off the critical path): held across the loop -- or hoisted out of the solve loop by
+                // loop-invariant code motion -- they would stay live through every other phase and push the kernel's
+                // long-lived state past the 256 registers of two waves per SIMD.
+                const bool want_S = mode == PRED;
+                d4 P;
+                {
+                    const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = lr + 4 * i;
+                        P[i] = (r == lc && r < 12) ? qw[r < 12 ? r : 0] : 0.0;
+                        if (lc == 12 && i < 3) P[i] = -qw[r] * xr[(H - 1) * 12 + r];
+                    }
+                }
+                // operands of stage k: B^ k-blocks 1-2 (rows 4+lr, 8+lr: Bt (S slot) in columns 0-11, dv in column
+                // 12), X = [0 | Bt' | rr] (columns 6-11: Bt[lc-6][row], column 12: rr[row] from the x slot), and
+                // the column 12 of Q^_k (-q x_ref,k-1); out-of-range lanes read the zero words
+                double bg[2], xg[3], qn[3];
+                auto fetch = [&](int k) {
+                    const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+#pragma unroll
+                    for (int kk = 0; kk < 2; ++kk) {
+                        const int r = 4 * (kk + 1) + lr;
+                        const bool in = r >= 6 && r < 12 && lc <= 12;
+                        const int off = lc < 12 ? LQ_S + (r - 6) * 12 + lc : LQ_DV + (r - 6);
+                        bg[kk] = (in ? sl : zero)[in ? off : 0];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const int r = lr + 4 * i;
+                        const bool in = lc >= 6 && lc <= 12;
+                        const int off = lc < 12 ? LQ_S + (lc - 6) * 12 + r : LQ_X + r;
+                        xg[i] = (in ? sl : zero)[in ? off : 0];
+                    }
+                    const int km = k > 0 ? k - 1 : 0;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) qn[i] = (lc == 12) ? -qw[lr + 4 * i] * xr[km * 12 + lr + 4 * i] : 0.0;
+                };
+                fetch(H - 1);
+                for (int k = H - 1; k >= 0; --k) {
+                    const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
+                    ldouble* sl = slots + k * LQ_SLOT;
+                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                    double bh[2], xb[3], qc[3];
+#pragma unroll
+                    for (int kk = 0; kk < 2; ++kk) bh[kk] = bg[kk];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        xb[i] = xg[i];
+                        qc[i] = qn[i];
+                    }
+                    // dt N(yaw_k), k-blocks 0-1 (rows 0-7) in the accumulator layout
+                    double nh[2];
+#pragma unroll
+                    for (int kk = 0; kk < 2; ++kk) nh[kk] = lq_dtN(4 * kk + lr, lc, ck, sk, dt);
+                    // C = P^ B^ ; PA = P^ A (the d column below) ; Guu = B^' C
+                    d4 C = {0.0, 0.0, 0.0, 0.0};
+                    C = MFMA64(P[1], bh[0], C);
+                    C = MFMA64(P[2], bh[1], C);
+                    d4 PA = P;
+                    PA = MFMA64(P[0], nh[0], PA);
+                    PA = MFMA64(P[1], nh[1], PA);
+                    d4 G = {0.0, 0.0, 0.0, 0.0};
+                    G = MFMA64(bh[0], C[1], G);
+                    G = MFMA64(bh[1], C[2], G);
+                    // next stage's operands, issued while the matrix cores work through the chain above
+                    __builtin_amdgcn_sched_barrier(0);
+                    fetch(k > 0 ? k - 1 : 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
+                    if (lc == 12) {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) PA[i] += C[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) (lc == 12 ? sl : sink)[lc == 12 ? LQ_V + lr + 4 * i : lane] = C[i];
+#pragma unroll
+                    for (int i = 1; i < 3; ++i) {
+                        const int r = lr + 4 * i;
+                        const bool o = r >= 6 && r < 12 && lc <= 12;
+                        (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : lane] = PA[i];
+                    }
+                    // ---- block Cholesky of Guu by legs, L^-1 and X = L^-1 [0 | Bt' | rr] alongside ----
+                    d4 Tg, Li, X;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = lr + 4 * i;
+                        Tg[i] = (r < 12 && lc < 12) ? G[i] : 0.0;
+                        Li[i] = (r == lc) ? 1.0 : 0.0;
+                        X[i] = (i < 3) ? xb[i < 3 ? i : 0] : 0.0;
+                    }
+                    const int ls0 = 4 * k;
+                    const int amask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
+#pragma unroll
+                    for (int blk = 0; blk < 4; ++blk) {
+                        if (!((amask >> blk) & 1)) continue;
+                        const int o = 3 * blk;
+                        const int i0 = o >> 2, i1 = (o + 2) >> 2;
+                        const int ra = 4 * i0 + lr - o, rb = 4 * i1 + lr - o;
+                        const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
+                        // Rr_j of this leg-step, from its lane (wave-uniform)
+                        const int srcl = (ls0 + blk) & 63, srct = (ls0 + blk) >> 6;
+                        double Rj[6];
+#pragma unroll
+                        for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
+                        LMPC_SYNC();
+                        {
+                            ldouble* da = ina ? pv + 16 * ra + lc : sink + lane;
+                            da[0] = Tg[i0];
+                            if (i1 != i0) {
+                                ldouble* db = inb ? pv + 16 * rb + lc : sink + lane;
+                                db[0] = Tg[i1];
+                            }
+                        }
+                        LMPC_SYNC();
+                        const double p00 = pv[o] + Rj[0], p10 = pv[16 + o] + Rj[1], p11 = pv[16 + o + 1] + Rj[3];
+                        const double p20 = pv[32 + o] + Rj[2], p21 = pv[32 + o + 1] + Rj[4], p22 = pv[32 + o + 2] + Rj[5];
+                        const double t0 = pv[lc], t1 = pv[16 + lc], t2 = pv[32 + lc];
+                        {
+                            ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + lane;
+                            da[0] = Li[i0];
+                            ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + lane;
+                            dx[0] = X[i0];
+                            Li[i0] = ina ? 0.0 : Li[i0];
+                            X[i0] = ina ? 0.0 : X[i0];
+                            if (i1 != i0) {
+                                ldouble* db = inb ? pv + 48 + 16 * rb + lc : sink + lane;
+                                db[0] = Li[i1];
+                                ldouble* dy = inb ? pv + 96 + 16 * rb + lc : sink + lane;
+                                dy[0] = X[i1];
+                                Li[i1] = inb ? 0.0 : Li[i1];
+                                X[i1] = inb ? 0.0 : X[i1];
+                            }
+                        }
+                        LMPC_SYNC();
+                        const double w0 = pv[48 + lc], w1 = pv[64 + lc], w2 = pv[80 + lc];
+                        const double y0 = pv[96 + lc], y1 = pv[112 + lc], y2 = pv[128 + lc];
+                        const double i00 = rsq_nr(p00);
+                        const double l10 = p10 * i00, l20 = p20 * i00;
+                        const double i11 = rsq_nr(fma(-l10, l10, p11));
+                        const double l21 = fma(-l20, l10, p21) * i11;
+                        const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
+                        const double x0 = t0 * i00;
+                        const double x1 = fma(-l10, x0, t1) * i11;
+                        const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
+                        const double xs = lr == 0 ? x0 : lr == 1 ? x1 : x2;
+                        const double av = (lc > o + 2 && lc < 12 && lr < 3) ? xs : 0.0;
+                        const double v0 = w0 * i00;
+                        const double v1 = fma(-l10, v0, w1) * i11;
+                        const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
+                        const double q0 = y0 * i00;
+                        const double q1 = fma(-l10, q0, y1) * i11;
+                        const double q2 = fma(-l21, q1, fma(-l20, q0, y2)) * i22;
+                        const double bw = lr == 0 ? v0 : lr == 1 ? v1 : lr == 2 ? v2 : 0.0;
+                        const double bx = lr == 0 ? q0 : lr == 1 ? q1 : lr == 2 ? q2 : 0.0;
+                        const bool cp = lc >= o && lc <= o + 2;
+                        const double aw = cp ? (lr == lc - o ? 1.0 : 0.0) : -av;
+                        Tg = MFMA64(-av, av, Tg);
+                        Li = MFMA64(aw, bw, Li);
+                        X = MFMA64(aw, bx, X);
+                    }
+                    // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
+                    d4 KH = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int kk = 0; kk < 3; ++kk) KH = MFMA64(X[kk], X[kk], KH);
+#pragma unroll
+                    for (int i = 1; i < 3; ++i) {
+                        const int r = lr + 4 * i;
+                        const bool zr = r >= 6 && r < 12;
+                        const bool ko = zr && ((lc >= 6 && lc < 12 && lc <= r) || lc == 12);
+                        const int off = lc == 12 ? LQ_RHO + (r - 6) : LQ_K + pk6(r - 6, lc - 6);
+                        (ko ? sl : sink)[ko ? off : lane] = KH[i];
+                    }
+                    if (k > 0) {
+                        // KZ = KH M' (k-blocks 1-2; M' = PA with row 12 = e12: its k = 12 term is KH column 12 added
+                        // to column 12 lane-locally)
+                        d4 KZ = {0.0, 0.0, 0.0, 0.0};
+                        KZ = MFMA64(KH[1], PA[1], KZ);
+                        KZ = MFMA64(KH[2], PA[2], KZ);
+                        if (lc == 12) {
+#pragma unroll
+                            for (int i = 0; i < 3; ++i) KZ[i] += KH[i];
+                        }
+                        // P^_k = Q^_k + A^'PA - M'KZ  (rows 0-11; row 12 is never read)
+                        d4 Pn;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int r = lr + 4 * i;
+                            const double qd = (r == lc && r < 12) ? qw[r < 12 ? r : 0] : 0.0;
+                            Pn[i] = PA[i] + qd + ((lc == 12 && i < 3) ? qc[i < 3 ? i : 0] : 0.0);
+                        }
+                        Pn = MFMA64(nh[0], PA[0], Pn);
+                        Pn = MFMA64(nh[1], PA[1], Pn);
+                        Pn = MFMA64(-PA[1], KZ[1], Pn);
+                        Pn = MFMA64(-PA[2], KZ[2], Pn);
+                        P = Pn;
+                    }
+                    if (want_S) {  // S = X'L^-1 rows 6-11 = Bt Guu^-1 (off the critical path)
+                        d4 SS = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int kk = 0; kk < 3; ++kk) SS = MFMA64(X[kk], Li[kk], SS);
+#pragma unroll
+                        for (int i = 1; i < 3; ++i) {
+                            const int r = lr + 4 * i;
+                            const bool so = r >= 6 && r < 12 && lc < 12;
+                            (so ? sl : sink)[so ? LQ_S + (r - 6) * 12 + lc : lane] = SS[i];
+                        }
+                    }
+                    // the pivot staging and the next stage's slot reads are ordered by the next LMPC_SYNC
+                }
+                LMPC_SYNC();
+                LQ_STAMP(3);  // factorisation
+            }
+
+#ifdef LMPC_LQ_DEBUG
+            if (qp == 0 && mode == PRED && ipm_it == 0) {  // QP 0's slots right after the first factorisation
+                LMPC_SYNC();
+                for (int e = lane; e < lq_lds_doubles(H) && e < 8192; e += 64) lmpc_lq_dbg2[e] = sm[e];
+            }
+#endif
+            // ======== forward sweep: w = Z x + za ; x' = A x + d - [0; K w + rho] ========
+            {
+                if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
+                LMPC_SYNC();
+                for (int k = 0; k < H; ++k) {
+                    // lane roles from an opaque lane index (addresses computed per stage, never hoisted)
+                    const int ln = lq_opaque(lane);
+                    const int m = ln < 24 ? (ln >> 2) : 0, part = ln & 3;  // w: lanes 4m..4m+3, 3 terms each
+                    const int r = ln < 12 ? ln : 0;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+                    const ldouble* x = ex + 16;
+                    double w = sl[LQ_Z + m * 13 + 3 * part] * x[3 * part];
+                    w = fma(sl[LQ_Z + m * 13 + 3 * part + 1], x[3 * part + 1], w);
+                    w = fma(sl[LQ_Z + m * 13 + 3 * part + 2], x[3 * part + 2], w);
+                    w = quad_sum(w) + sl[LQ_Z + m * 13 + 12];
+                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                    // w_m to every lane (readlane in uniform control flow: all lanes take part in the DPP sums
+                    // above, and the broadcast reads lanes 0, 4, ..., 20)
+                    double wb[6];
+#pragma unroll
+                    for (int mm = 0; mm < 6; ++mm) wb[mm] = readlane_f64(w, 4 * mm);
+                    const int a = r >= 6 ? r - 6 : 0;
+                    double kw = sl[LQ_DV + a] - sl[LQ_RHO + a];
+#pragma unroll
+                    for (int mm = 0; mm < 6; ++mm) kw = fma(-sl[LQ_K + pk6(a, mm)], wb[mm], kw);
+                    const double xn = lq_Ax(x, r, ck, sk, dt, 1.0) + (r >= 6 ? kw : 0.0);
+                    LMPC_SYNC();
+                    if (lane < 12) {
+                        ex[16 + r] = xn;
+                        slots[k * LQ_SLOT + LQ_X + r] = xn;
+                    }
+                    LMPC_SYNC();
+                }
+            }
+            LQ_STAMP(4);  // forward sweep
+            // ======== inputs from the costate: lambda2 = Z A^-1 x' + za - v2 (-> rho slot), then per leg-step ========
+            {
+                constexpr int NT6 = (6 * LMPC_MAX_HORIZON + 63) / 64;
+#pragma unroll
+                for (int i = 0; i < NT6; ++i) {
+                    const int e = lane + 64 * i;
+                    if (64 * i >= 6 * H) break;  // wave-uniform
+                    const int ec = e < 6 * H ? e : 6 * H - 1;
+                    const int k = ec / 6, m = ec - 6 * k;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+                    const ldouble* xk = sl + LQ_X;
+                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                    double lam = sl[LQ_Z + m * 13 + 12] - sl[LQ_V + 6 + m];
+#pragma unroll
+                    for (int c = 0; c < 12; ++c) lam = fma(sl[LQ_Z + m * 13 + c], lq_Ax(xk, c, ck, sk, dt, -1.0), lam);
+                    if (e < 6 * H) slots[k * LQ_SLOT + LQ_RHO + m] = lam;
+                }
+                LMPC_SYNC();
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    u[t][0] = u[t][1] = u[t][2] = 0.0;
+                    if (!st[t]) continue;
+                    const int j = lsj[t];
+                    const ldouble* lam = slots + lsk[t] * LQ_SLOT + LQ_RHO;
+                    double l2[6];
+#pragma unroll
+                    for (int mm = 0; mm < 6; ++mm) l2[mm] = lam[mm];
+                    // b = rr + T' G0_j' lambda2 ; y = -Rr^-1 b ; u = up + T y
+                    double gj[3], b[3], y[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) v = fma(G0s[mm * 12 + 3 * j + p], l2[mm], v);
+                        gj[p] = v;
+                    }
+                    double T[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, up[3] = {0.0, 0.0, 0.0};
+                    if (mode == POLISH) (void)leg_basis(act[t], mu, fzmax, T, up);
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) b[a] = -(rr[t][a] + T[0 * 3 + a] * gj[0] + T[1 * 3 + a] * gj[1] + T[2 * 3 + a] * gj[2]);
+                    sym3_solve(Rr[t], b, y);
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) u[t][p] = up[p] + T[p * 3] * y[0] + T[p * 3 + 1] * y[1] + T[p * 3 + 2] * y[2];
+                }
+            }
+            LQ_STAMP(5);  // inputs
+#ifdef LMPC_LQ_DEBUG
+            // diagnostic build only: QP 0's LDS and inputs after the first predictor solve (tools/lq_debug.py)
+            if (qp == 0 && mode == PRED && ipm_it == 0) {
+                LMPC_SYNC();
+                for (int e = lane; e < lq_lds_doubles(H) && e < 8192; e += 64) lmpc_lq_dbg[e] = sm[e];
+#pragma unroll
+                for (int t = 0; t < LS; ++t)
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) lmpc_lq_dbg_u[(lane + 64 * t) * 3 + m] = u[t][m];
+            }
+#endif
+
+            if (mode == PRED) {
+                double amax = 1.0;
+                double dsa[LS][5], dza[LS][5];
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) dsa[t][i] = dza[t][i] = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) ua[t][m] = u[t][m];
+                    if (!st[t]) continue;
+                    double o[5];
+                    cons_resid(u[t], mu, fzmax, o);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        dsa[t][i] = -o[i] - s[t][i];
+                        dza[t][i] = -z[t][i] - z[t][i] * rcp_nr(s[t][i]) * dsa[t][i];
+                        if (dsa[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(dsa[t][i]));
+                        if (dza[t][i] < 0.0) amax = fmin(amax, -z[t][i] * __builtin_amdgcn_rcp(dza[t][i]));
+                    }
+                }
+                const double aa = wave_min(amax);
+                double loc = 0.0;
+#pragma unroll
+                for (int t = 0; t < LS; ++t)
+                    if (st[t])
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) loc += (s[t][i] + aa * dsa[t][i]) * (z[t][i] + aa * dza[t][i]);
+                const double ratio = (wave_sum(loc) / mc) / mu_c;
+                smu = ratio * ratio * ratio * mu_c;
+                // corrector linear term rr' = C' w'
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    if (!st[t]) continue;
+                    double wv[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+                        wv[i] = (z[t][i] * (s[t][i] - (i == 4 ? fzmax : 0.0)) + smu - dsa[t][i] * dza[t][i]) * rcp_nr(s[t][i]);
+                    cons_tw(wv, mu, rr[t]);
+                }
+                mode = CORR;
+                LQ_STAMP(6);  // predictor step
+            } else if (mode == CORR) {
+                double ds[LS][5], dz[LS][5];
+                double amax = 1.0, dmax = 1.0;
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) ds[t][i] = dz[t][i] = 0.0;
+                    if (!st[t]) continue;
+                    double o[5], oa[5];
+                    cons_resid(u[t], mu, fzmax, o);
+                    cons_resid(ua[t], mu, fzmax, oa);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        const double is = rcp_nr(s[t][i]);
+                        const double dsa = -oa[i] - s[t][i];
+                        const double dza = -z[t][i] - z[t][i] * is * dsa;
+                        ds[t][i] = -o[i] - s[t][i];
+                        dz[t][i] = (smu - z[t][i] * s[t][i] - dsa * dza - z[t][i] * ds[t][i]) * is;
+                        if (ds[t][i] < 0.0) amax = fmin(amax, -s[t][i] * __builtin_amdgcn_rcp(ds[t][i]));
+                        if (dz[t][i] < 0.0) dmax = fmin(dmax, -z[t][i] * __builtin_amdgcn_rcp(dz[t][i]));
+                    }
+                }
+#if LMPC_SPLIT_STEP
+                const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
+                const double alpd = fmin(1.0, LMPC_STEP_FRAC * wave_min(dmax));
+#else
+                const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(fmin(amax, dmax))), alpd = alpha;
+#endif
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    if (!st[t]) continue;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) f[t][m] += alpha * (u[t][m] - f[t][m]);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        s[t][i] += alpha * ds[t][i];
+                        z[t][i] += alpd * dz[t][i];
+                    }
+                }
+                ++ipm_it;
+                mode = PRED;
+                LQ_STAMP(7);  // corrector step
+            } else {
+                ++prounds;
+                // ======== polish verification: the adjoint lambda from the trajectory (independent of the
+                // factorisation), then primal feasibility and multiplier signs (lmpc_kernels.hip) ========
+                {
+                    // tracking terms q (x_k - x_ref,k-1) of every stage at once -> x slot (dead after this), then the
+                    // serial sweep lambda_k = q_k-term + A_k' lambda_{k+1}, lambda_{k+1}[6:12] -> rho slot k
+                    const int r = lane < 12 ? lane : 0;
+                    double lam = lane < 12 ? qw[r] * (slots[(H - 1) * LQ_SLOT + LQ_X + r] - xr[(H - 1) * 12 + r]) : 0.0;
+                    for (int k = H - 1; k >= 0; --k) {
+                        if (lane < 12) ex[r] = lam;
+                        if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_RHO + (lane - 6)] = lam;
+                        LMPC_SYNC();
+                        if (k == 0) break;
+                        const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                        lam = qw[r] * (slots[(k - 1) * LQ_SLOT + LQ_X + r] - xr[(k - 1) * 12 + r]) + lq_Atw(ex, r, ck, sk, dt);
+                        LMPC_SYNC();
+                    }
+                }
+                LQ_STAMP(8);  // adjoint
+                double g[LS][3];
+                double gloc = 1.0;
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    g[t][0] = g[t][1] = g[t][2] = 0.0;
+                    if (!valid[t]) continue;
+                    const int j = lsj[t];
+                    const ldouble* lam = slots + lsk[t] * LQ_SLOT + LQ_RHO;
+                    double ru[3];
+                    if constexpr (!TERRAIN) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) ru[p] = prm.r[3 * j + p] * u[t][p];
+                    } else {
+                        const ldouble* rb = rbt + 6 * j;
+                        ru[0] = rb[0] * u[t][0] + rb[1] * u[t][1] + rb[2] * u[t][2];
+                        ru[1] = rb[1] * u[t][0] + rb[3] * u[t][1] + rb[4] * u[t][2];
+                        ru[2] = rb[2] * u[t][0] + rb[4] * u[t][1] + rb[5] * u[t][2];
+                    }
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        double v = ru[p];
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) v += G0s[m * 12 + 3 * j + p] * lam[m];
+                        g[t][p] = v;
+                        gloc = fmax(gloc, fabs(v));
+                    }
+                }
+                const double gscale = wave_max(gloc);
+                int changed = 0;
+#pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    if (!st[t]) continue;
+                    double o[5];
+                    cons_resid(u[t], mu, fzmax, o);
+                    int imax = -1;
+                    double vmax = prm.tol_p * fzmax;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+                        if (!((act[t] >> i) & 1) && o[i] > vmax) {
+                            vmax = o[i];
+                            imax = i;
+                        }
+                    if (imax >= 0) {
+                        act[t] |= 1 << imax;
+                        changed = 1;
+                        continue;
+                    }
+                    if (apex[t]) {
+                        if (g[t][2] / mu < fabs(g[t][0]) + fabs(g[t][1]) - prm.tol_d * gscale) {
+                            act[t] = (g[t][0] < 0.0 ? 2 : 1) | (g[t][1] < 0.0 ? 8 : 4);
+                            changed = 1;
+                        }
+                        continue;
+                    }
+                    if (act[t] == 0) continue;
+                    const int df = leg_drop_face(act[t], g[t], mu, -prm.tol_d * gscale);
+                    if (df >= 0) {
+                        act[t] &= ~(1 << df);
+                        changed = 1;
+                    }
+                }
+                LQ_STAMP(9);  // polish verification
+                if (!__any(changed)) {
+                    done = true;
+                    break;
+                }
+                if (++rd >= prm.max_rounds) {
+                    if (++att >= prm.max_attempts) break;
+                    tol = retry_tol(tol, att);
+                    it_end += prm.max_iter;
+                    mode = PRED;
+                }
+            }
+        }
+    } else {
+        done = true;
+    }
+    if (!done) {
+        qstatus = LMPC_QP_MAX_ITER;  // no verified active set: the (feasible) interior-point iterate
+#pragma unroll
+        for (int t = 0; t < LS; ++t)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) u[t][m] = f[t][m];
+    }
+    // ---- NaN guard (reference: NaN -> zeros, ConvexQPSolver.cpp:321-326) and output ----
+    int bad = 0;
+#pragma unroll
+    for (int t = 0; t < LS; ++t)
+        if (valid[t]) bad |= (u[t][0] != u[t][0] || u[t][1] != u[t][1] || u[t][2] != u[t][2]) ? 1 : 0;
+    const bool anybad = __any(bad);
+    double* gout = grf + (size_t)qp * 12 * H;
+#pragma unroll
+    for (int t = 0; t < LS; ++t) {
+        if (!valid[t]) continue;
+        const int ls = lane + 64 * t;
+        double fo[3] = {u[t][0], u[t][1], u[t][2]};
+        if constexpr (TERRAIN) {
+            const ldouble* Rj = tf + 9 * lsj[t];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) fo[p] = Rj[3 * p] * u[t][0] + Rj[3 * p + 1] * u[t][1] + Rj[3 * p + 2] * u[t][2];
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) gout[3 * ls + p] = (anybad || !st[t]) ? 0.0 : fo[p];
+    }
+    if (lane == 0) {
+        if (status) status[qp] = anybad ? LMPC_QP_NAN : qstatus;
+        if (iters) iters[qp] = ipm_it | (prounds << 16);
+    }
+    LQ_STAMP(10);
+    LQ_STAMP_FLUSH(qp);
+}
+
+#define LMPC_LQ_INST(LS_, T_)                                                                                    \
+    template __global__ void lmpc_lq_kernel<LS_, T_>(const DevParams, const double*, const uint8_t*, const double*, \
+                                                     int, double*, int32_t*, int32_t*, const uint8_t*);
+LMPC_LQ_INST(1, false)
+LMPC_LQ_INST(2, false)
+LMPC_LQ_INST(1, true)
+LMPC_LQ_INST(2, true)
+#undef LMPC_LQ_INST
+
+template <int LS, bool TERRAIN>
+static void launch_lq_variant(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                              int batch, double* grf, int32_t* status, int32_t* iters, const uint8_t* done,
+                              hipStream_t stream) {
+    const size_t lds = lq_lds_bytes(prm.H);
+    (void)hipFuncSetAttribute((const void*)lmpc_lq_kernel<LS, TERRAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL((lmpc_lq_kernel<LS, TERRAIN>), dim3(batch), dim3(LMPC_WAVE), lds, stream, prm, rec, contact,
+                       normals, batch, grf, status, iters, done);
+}
+
+// Host-side launcher (lmpc_capi.cpp): cold solves of every QP the dense kernel did not take.
+hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals, int batch,
+                     double* grf, int32_t* status, int32_t* iters, const uint8_t* done, hipStream_t stream) {
+    const bool two = 4 * prm.H > 64;
+    if (normals) {
+        if (two) launch_lq_variant<2, true>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
+        else launch_lq_variant<1, true>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
+    } else {
+        if (two) launch_lq_variant<2, false>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
+        else launch_lq_variant<1, false>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
+    }
+    return hipGetLastError();
+}
+
+#ifdef LMPC_STAMPS
+extern "C" int lmpc_debug_lq_stamps(unsigned long long* out, int nqp) {
+    if (nqp > LQ_STAMP_QPS) nqp = LQ_STAMP_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_lq_stamps), (size_t)nqp * LQ_STAMP_N * sizeof(unsigned long long)) ==
+                   hipSuccess ? nqp : -1;
+}
+#endif
+
+}  // namespace lmpc

@@ -64,10 +64,13 @@ class BatchedConvexQPSolver:
     """A device context: horizon H, host staging for up to max_batch QPs."""
 
     DENSE_PATHS = {"off": 0, "ipm": 1, "gi": 2}
+    RICCATI_PATHS = {"scratch": 0, "lds": 1}
 
     def __init__(self, params: N.LmpcParams, horizon: int, max_batch: int = 1, device: int = 0,
-                 options: N.LmpcOptions | None = None, dense_path: str | None = None):
-        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path)."""
+                 options: N.LmpcOptions | None = None, dense_path: str | None = None,
+                 riccati_path: str | None = None):
+        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path); riccati_path: "lds" (default, the
+        LDS-resident kernel) or "scratch" (the global-workspace kernel) -- lmpc_set_riccati_path."""
         if not (1 <= horizon <= N.LMPC_MAX_HORIZON):
             raise ValueError(f"horizon must be in [1, {N.LMPC_MAX_HORIZON}]")
         self._L = N.lib()
@@ -81,6 +84,16 @@ class BatchedConvexQPSolver:
             self.set_options(options)
         if dense_path is not None:
             self.set_dense_path(dense_path)
+        if riccati_path is not None:
+            self.set_riccati_path(riccati_path)
+
+    def set_riccati_path(self, path: str) -> None:
+        N.check(self._L.lmpc_set_riccati_path(self._ctx, self.RICCATI_PATHS[path]), "lmpc_set_riccati_path")
+
+    @property
+    def riccati_path(self) -> str:
+        """The Riccati kernel of cold solves for this context."""
+        return {0: "scratch", 1: "lds"}[self._L.lmpc_get_riccati_path(self._ctx)]
 
     def set_dense_path(self, path: str) -> None:
         N.check(self._L.lmpc_set_dense_path(self._ctx, self.DENSE_PATHS[path]), "lmpc_set_dense_path")

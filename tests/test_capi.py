@@ -38,7 +38,7 @@ def test_exports_are_c_linkage():
 
 def test_abi_and_strings():
     lib = N.lib()
-    assert lib.lmpc_abi_version() == 5
+    assert lib.lmpc_abi_version() == 6
     assert lib.lmpc_record_len(10) == 153 and lib.lmpc_record_len(30) == 393
     assert lib.lmpc_strerror(0) == b"ok"
     assert lib.lmpc_strerror(-1) == b"invalid argument"

@@ -28,7 +28,7 @@ def rows(name):
     return list(csv.DictReader(open(os.path.join(SRC, name, f"{name}_counter_collection.csv"))))
 
 
-SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_gi_kernel", "lmpc_qp_kernel")  # one solve launch = a dense-path kernel + the Riccati kernel
+SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_gi_kernel", "lmpc_qp_kernel", "lmpc_lq_kernel")  # one solve launch = a dense-path kernel + the Riccati kernel
 
 
 def per_kernel(name, kern, counter=None):
