@@ -40,7 +40,7 @@ namespace lmpc {
 
 #ifdef LMPC_STAMPS
 constexpr int LQ_STAMP_QPS = 4096;
-constexpr int LQ_STAMP_N = 12;
+constexpr int LQ_STAMP_N = 16;
 __device__ unsigned long long lmpc_lq_stamps[LQ_STAMP_QPS][LQ_STAMP_N];
 #define LQ_STAMP_DECL unsigned long long _lq_acc[LQ_STAMP_N] = {}; unsigned long long _lq_t0 = __builtin_readcyclecounter();
 #define LQ_STAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _lq_acc[i] += _t - _lq_t0; _lq_t0 = _t; } while (0)
@@ -93,20 +93,15 @@ __device__ __forceinline__ constexpr int pk6(int a, int b) {  // packed lower 6x
 
 // entries of dt N(yaw) = A_k - I (rows 0-5, columns 6-11)
 __device__ __forceinline__ double lq_dtN(int r, int c, double ck, double sk, double dt) {
-    if (r >= 12 || c >= 12) return 0.0;
-    double v = 0.0;
-    if (r < 3 && c >= 6 && c < 9) {
-        const int j = c - 6;
-        const double m = (r == 0) ? ((j == 0) ? ck : (j == 1) ? sk : 0.0)
-                       : (r == 1) ? ((j == 0) ? -sk : (j == 1) ? ck : 0.0)
-                                  : ((j == 2) ? 1.0 : 0.0);
-        v += dt * m;
-    }
-    if (r >= 3 && r < 6 && c == r + 6) v += dt;
-    return v;
+    // lane-static pattern: rows 0-1 x columns 6-7 the yaw rotation, (2, 8) and (r, r + 6) for r = 3..5 one
+    const bool rot = r < 2 && (c == 6 || c == 7);
+    const bool one = (r == 2 && c == 8) || (r >= 3 && r < 6 && c == r + 6);
+    const bool cs_ = (r == 0) == (c == 6);  // (0,6), (1,7): cos; (0,7), (1,6): +-sin
+    const double rv = cs_ ? ck : (r == 0 ? sk : -sk);
+    return dt * (rot ? rv : (one ? 1.0 : 0.0));
 }
 
-// (A x)[r], (A^-1 x)[r] (A = I + dt N, N nilpotent: A^-1 = I - dt N), (A' w)[r]
+// (A x)[r], (A^-1 x)[r] (A = I + dt N, N nilpotent: A^-1 = I - dt N) for a compile-time row r
 template <class Ptr>
 __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, double dt, double sgn) {
     if (r == 0) return x[0] + sgn * dt * (ck * x[6] + sk * x[7]);
@@ -115,18 +110,38 @@ __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, doub
     if (r < 6) return x[r] + sgn * dt * x[r + 6];
     return x[r];
 }
-template <class Ptr>
-__device__ __forceinline__ double lq_Atw(Ptr w, int r, double ck, double sk, double dt) {
-    if (r == 6) return w[6] + dt * (ck * w[0] - sk * w[1]);
-    if (r == 7) return w[7] + dt * (sk * w[0] + ck * w[1]);
-    if (r == 8) return w[8] + dt * w[2];
-    if (r >= 9) return w[r] + dt * w[r - 6];
-    return w[r];
-}
 
 __device__ __forceinline__ int lq_opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
+}
+
+// The same products branch-free for a runtime row r: (A x)[r] = x[r] + dt (a1 x[c1] + a2 x[c2]) and
+// (A' w)[r] = w[r] + dt (a1 w[c1] + a2 w[c2]), with lane-static columns and coefficients selected from (cos, sin)
+// of the stage's yaw; every operand load is unconditional (a divergent branch per row waits on its own loads).
+struct LqRow {
+    int c1, c2;
+    double a1, a2;
+};
+__device__ __forceinline__ LqRow lq_ax_row(int r, double ck, double sk) {
+    LqRow o;
+    o.c1 = r < 2 ? 6 : (r < 6 ? r + 6 : 6);
+    o.c2 = 7;
+    o.a1 = r == 0 ? ck : r == 1 ? -sk : (r < 6 ? 1.0 : 0.0);
+    o.a2 = r == 0 ? sk : r == 1 ? ck : 0.0;
+    return o;
+}
+__device__ __forceinline__ LqRow lq_atw_row(int r, double ck, double sk) {
+    LqRow o;
+    o.c1 = r >= 8 ? r - 6 : 0;
+    o.c2 = 1;
+    o.a1 = r == 6 ? ck : r == 7 ? sk : (r >= 8 ? 1.0 : 0.0);
+    o.a2 = r == 6 ? -sk : r == 7 ? ck : 0.0;
+    return o;
+}
+template <class Ptr>
+__device__ __forceinline__ double lq_row_apply(Ptr x, int r, const LqRow& q, double s) {
+    return fma(s, fma(q.a1, x[q.c1], q.a2 * x[q.c2]), x[r]);
 }
 
 // lane-local solve of the symmetric positive definite 3x3 system R y = b (R packed [xx xy xz yy yz zz])
@@ -146,10 +161,11 @@ __device__ __forceinline__ void sym3_solve(const double R[6], const double b[3],
 
 // ---------------------------------------------------------------------------------------------------------
 // The kernel.  LS = leg-steps per lane (ceil(4H/64)); TERRAIN: per-leg contact frames (lmpc_kernels.hip).
-// Two waves per SIMD at LS = 1 (256 registers), one at LS = 2.
+// WPE = waves per SIMD the register budget allows: 2 (256 registers, LS = 1 only: eight QPs per CU at H <= 10) or 1
+// (512, no spills: the instance for batches of at most one QP per SIMD, and for LS = 2).
 // ---------------------------------------------------------------------------------------------------------
-template <int LS, bool TERRAIN>
-__global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevParams prm, const double* __restrict__ rec,
+template <int LS, bool TERRAIN, int WPE>
+__global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, const double* __restrict__ rec,
                                                                      const uint8_t* __restrict__ contact,
                                                                      const double* __restrict__ normals, int batch,
                                                                      double* __restrict__ grf, int32_t* __restrict__ status,
@@ -344,6 +360,13 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
             // stage data per leg-step: Rr (the input Hessian block), rr (linear term), and for the factorisation
             // Bt = G0_j T -> S slot, rr -> x slot, G0_j up (-> dv) with T the leg's null-space basis (I for a stance leg
             // in the interior point, 0 for a swing leg) and up its particular solution (polish only)
+            // the tracking terms -Q x_ref,j of every stage, loaded from the record here (global memory: every load
+            // issued at once, ahead of the leg-step work) and stored to slot j below -- v field before a
+            // factorisation, x field before the corrector's backward sweep -- so the serial sweeps read LDS only
+            constexpr int NTQ = LS == 1 ? 3 : 6;
+            double qxl[NTQ];
+#pragma unroll
+            for (int i = 0; i < NTQ; ++i) qxl[i] = xr[min(lane + 64 * i, 12 * H - 1)];
             double du[LS][6];
             bool cpl[LS];
 #pragma unroll
@@ -442,6 +465,14 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
             unsigned long long cmask[LS];
 #pragma unroll
             for (int t = 0; t < LS; ++t) cmask[t] = __ballot(cpl[t]);
+            {
+                const int fld = mode == CORR ? LQ_X : LQ_V;
+#pragma unroll
+                for (int i = 0; i < NTQ; ++i) {
+                    const int e = lane + 64 * i, j = e / 12, r = e - 12 * j;
+                    if (e < 12 * H) slots[j * LQ_SLOT + fld + r] = -qw[r] * qxl[i];
+                }
+            }
             LMPC_SYNC();
             LQ_STAMP(1);  // leg-step work
 
@@ -469,7 +500,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                 // Lanes 0-11 hold p (lane r <-> p[r]); y goes through the exchange buffer, t by readlane.
                 {
                     const int r = lane < 12 ? lane : 0;
-                    double p = lane < 12 ? -qw[r] * xr[(H - 1) * 12 + r] : 0.0;
+                    double p = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
                     for (int k = H - 1; k >= 0; --k) {
                         const ldouble* sl = slots + k * LQ_SLOT;
                         const double y = p + sl[LQ_V + r];
@@ -483,7 +514,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
 #pragma unroll
                         for (int n = 0; n < 6; ++n) tv = fma(sl[LQ_K + pk6(m, n)], ex[6 + n], tv);
                         const double ck = cs[2 * k], sk = cs[2 * k + 1];
-                        double pn = -qw[r] * xr[(k - 1) * 12 + r] + lq_Atw(ex, r, ck, sk, dt);
+                        double pn = slots[(k - 1) * LQ_SLOT + LQ_X + r] + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
 #pragma unroll
                         for (int mm = 0; mm < 6; ++mm) pn = fma(-sl[LQ_Z + mm * 13 + r], readlane_f64(tv, mm), pn);
                         p = pn;
@@ -505,16 +536,18 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                     for (int i = 0; i < 4; ++i) {
                         const int r = lr + 4 * i;
                         P[i] = (r == lc && r < 12) ? qw[r < 12 ? r : 0] : 0.0;
-                        if (lc == 12 && i < 3) P[i] = -qw[r] * xr[(H - 1) * 12 + r];
+                        if (lc == 12 && i < 3) P[i] = slots[(H - 1) * LQ_SLOT + LQ_V + r];
                     }
                 }
                 // operands of stage k: B^ k-blocks 1-2 (rows 4+lr, 8+lr: Bt (S slot) in columns 0-11, dv in column
                 // 12), X = [0 | Bt' | rr] (columns 6-11: Bt[lc-6][row], column 12: rr[row] from the x slot), and
                 // the column 12 of Q^_k (-q x_ref,k-1); out-of-range lanes read the zero words
-                double bg[2], xg[3], qn[3];
+                double bg[2], xg[3], qn[3], ckn, skn;
                 auto fetch = [&](int k) {
                     const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
                     const ldouble* sl = slots + k * LQ_SLOT;
+                    ckn = cs[2 * k];
+                    skn = cs[2 * k + 1];
 #pragma unroll
                     for (int kk = 0; kk < 2; ++kk) {
                         const int r = 4 * (kk + 1) + lr;
@@ -531,13 +564,16 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                     }
                     const int km = k > 0 ? k - 1 : 0;
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) qn[i] = (lc == 12) ? -qw[lr + 4 * i] * xr[km * 12 + lr + 4 * i] : 0.0;
+                    for (int i = 0; i < 3; ++i) {
+                        const double qv = slots[km * LQ_SLOT + LQ_V + lr + 4 * i];
+                        qn[i] = lc == 12 ? qv : 0.0;
+                    }
                 };
                 fetch(H - 1);
                 for (int k = H - 1; k >= 0; --k) {
                     const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
                     ldouble* sl = slots + k * LQ_SLOT;
-                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                    const double ck = ckn, sk = skn;
                     double bh[2], xb[3], qc[3];
 #pragma unroll
                     for (int kk = 0; kk < 2; ++kk) bh[kk] = bg[kk];
@@ -549,7 +585,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                     // dt N(yaw_k), k-blocks 0-1 (rows 0-7) in the accumulator layout
                     double nh[2];
 #pragma unroll
-                    for (int kk = 0; kk < 2; ++kk) nh[kk] = lq_dtN(4 * kk + lr, lc, ck, sk, dt);
+                    for (int kk = 0; kk < 2; ++kk) nh[kk] = lq_dtN(4 * kk + lr, lc, ck, sk, dt);  // selects, no branches
                     // C = P^ B^ ; PA = P^ A (the d column below) ; Guu = B^' C
                     d4 C = {0.0, 0.0, 0.0, 0.0};
                     C = MFMA64(P[1], bh[0], C);
@@ -577,6 +613,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                         const bool o = r >= 6 && r < 12 && lc <= 12;
                         (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : lane] = PA[i];
                     }
+                    LQ_STAMP(11);  // factorisation: C, PA, G, Z / v stores
                     // ---- block Cholesky of Guu by legs, L^-1 and X = L^-1 [0 | Bt' | rr] alongside ----
                     d4 Tg, Li, X;
 #pragma unroll
@@ -600,20 +637,16 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                         double Rj[6];
 #pragma unroll
                         for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
+                        // the three tiles' pivot rows through LDS in one round trip (the fence ahead orders the
+                        // previous block's reads of the staging rows before these writes)
                         LMPC_SYNC();
                         {
-                            ldouble* da = ina ? pv + 16 * ra + lc : sink + lane;
-                            da[0] = Tg[i0];
+                            ldouble* dt0 = ina ? pv + 16 * ra + lc : sink + lane;
+                            dt0[0] = Tg[i0];
                             if (i1 != i0) {
-                                ldouble* db = inb ? pv + 16 * rb + lc : sink + lane;
-                                db[0] = Tg[i1];
+                                ldouble* dt1 = inb ? pv + 16 * rb + lc : sink + lane;
+                                dt1[0] = Tg[i1];
                             }
-                        }
-                        LMPC_SYNC();
-                        const double p00 = pv[o] + Rj[0], p10 = pv[16 + o] + Rj[1], p11 = pv[16 + o + 1] + Rj[3];
-                        const double p20 = pv[32 + o] + Rj[2], p21 = pv[32 + o + 1] + Rj[4], p22 = pv[32 + o + 2] + Rj[5];
-                        const double t0 = pv[lc], t1 = pv[16 + lc], t2 = pv[32 + lc];
-                        {
                             ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + lane;
                             da[0] = Li[i0];
                             ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + lane;
@@ -630,6 +663,9 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                             }
                         }
                         LMPC_SYNC();
+                        const double p00 = pv[o] + Rj[0], p10 = pv[16 + o] + Rj[1], p11 = pv[16 + o + 1] + Rj[3];
+                        const double p20 = pv[32 + o] + Rj[2], p21 = pv[32 + o + 1] + Rj[4], p22 = pv[32 + o + 2] + Rj[5];
+                        const double t0 = pv[lc], t1 = pv[16 + lc], t2 = pv[32 + lc];
                         const double w0 = pv[48 + lc], w1 = pv[64 + lc], w2 = pv[80 + lc];
                         const double y0 = pv[96 + lc], y1 = pv[112 + lc], y2 = pv[128 + lc];
                         const double i00 = rsq_nr(p00);
@@ -656,6 +692,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                         Li = MFMA64(aw, bw, Li);
                         X = MFMA64(aw, bx, X);
                     }
+                    LQ_STAMP(12);  // factorisation: leg blocks
                     // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
                     d4 KH = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -668,6 +705,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                         const int off = lc == 12 ? LQ_RHO + (r - 6) : LQ_K + pk6(r - 6, lc - 6);
                         (ko ? sl : sink)[ko ? off : lane] = KH[i];
                     }
+                    LQ_STAMP(13);  // factorisation: KH, K / rho stores
                     if (k > 0) {
                         // KZ = KH M' (k-blocks 1-2; M' = PA with row 12 = e12: its k = 12 term is KH column 12 added
                         // to column 12 lane-locally)
@@ -692,6 +730,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                         Pn = MFMA64(-PA[2], KZ[2], Pn);
                         P = Pn;
                     }
+                    LQ_STAMP(14);  // factorisation: KZ, P
                     if (want_S) {  // S = X'L^-1 rows 6-11 = Bt Guu^-1 (off the critical path)
                         d4 SS = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -703,6 +742,7 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                             (so ? sl : sink)[so ? LQ_S + (r - 6) * 12 + lc : lane] = SS[i];
                         }
                     }
+                    LQ_STAMP(15);  // factorisation: S
                     // the pivot staging and the next stage's slot reads are ordered by the next LMPC_SYNC
                 }
                 LMPC_SYNC();
@@ -726,21 +766,31 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                     const int r = ln < 12 ? ln : 0;
                     const ldouble* sl = slots + k * LQ_SLOT;
                     const ldouble* x = ex + 16;
+                    const int a = r >= 6 ? r - 6 : 0;
+                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                    // every operand of the stage is loaded up front; only x waits on the previous stage
+                    double kr[6];
+#pragma unroll
+                    for (int mm = 0; mm < 6; ++mm) kr[mm] = sl[LQ_K + pk6(a, mm)];
+                    const double base = sl[LQ_DV + a] - sl[LQ_RHO + a];
                     double w = sl[LQ_Z + m * 13 + 3 * part] * x[3 * part];
                     w = fma(sl[LQ_Z + m * 13 + 3 * part + 1], x[3 * part + 1], w);
                     w = fma(sl[LQ_Z + m * 13 + 3 * part + 2], x[3 * part + 2], w);
+                    const double xa = lq_row_apply(x, r, lq_ax_row(r, ck, sk), dt);
                     w = quad_sum(w) + sl[LQ_Z + m * 13 + 12];
-                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
                     // w_m to every lane (readlane in uniform control flow: all lanes take part in the DPP sums
                     // above, and the broadcast reads lanes 0, 4, ..., 20)
                     double wb[6];
 #pragma unroll
                     for (int mm = 0; mm < 6; ++mm) wb[mm] = readlane_f64(w, 4 * mm);
-                    const int a = r >= 6 ? r - 6 : 0;
-                    double kw = sl[LQ_DV + a] - sl[LQ_RHO + a];
+                    // K w in two independent halves (a shorter dependent chain)
+                    double k0 = base, k1 = 0.0;
 #pragma unroll
-                    for (int mm = 0; mm < 6; ++mm) kw = fma(-sl[LQ_K + pk6(a, mm)], wb[mm], kw);
-                    const double xn = lq_Ax(x, r, ck, sk, dt, 1.0) + (r >= 6 ? kw : 0.0);
+                    for (int mm = 0; mm < 3; ++mm) {
+                        k0 = fma(-kr[mm], wb[mm], k0);
+                        k1 = fma(-kr[mm + 3], wb[mm + 3], k1);
+                    }
+                    const double xn = xa + (r >= 6 ? k0 + k1 : 0.0);
                     LMPC_SYNC();
                     if (lane < 12) {
                         ex[16 + r] = xn;
@@ -899,14 +949,29 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
                     // tracking terms q (x_k - x_ref,k-1) of every stage at once -> x slot (dead after this), then the
                     // serial sweep lambda_k = q_k-term + A_k' lambda_{k+1}, lambda_{k+1}[6:12] -> rho slot k
                     const int r = lane < 12 ? lane : 0;
-                    double lam = lane < 12 ? qw[r] * (slots[(H - 1) * LQ_SLOT + LQ_X + r] - xr[(H - 1) * 12 + r]) : 0.0;
+                    {
+                        constexpr int NTQ = LS == 1 ? 3 : 6;
+                        double xl[NTQ];
+#pragma unroll
+                        for (int i = 0; i < NTQ; ++i) xl[i] = xr[min(lane + 64 * i, 12 * H - 1)];
+#pragma unroll
+                        for (int i = 0; i < NTQ; ++i) {
+                            const int e = lane + 64 * i, j = e / 12, rr_ = e - 12 * j;
+                            if (e < 12 * H) {
+                                ldouble* xs = slots + j * LQ_SLOT + LQ_X + rr_;
+                                xs[0] = qw[rr_] * (xs[0] - xl[i]);
+                            }
+                        }
+                        LMPC_SYNC();
+                    }
+                    double lam = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
                     for (int k = H - 1; k >= 0; --k) {
                         if (lane < 12) ex[r] = lam;
                         if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_RHO + (lane - 6)] = lam;
                         LMPC_SYNC();
                         if (k == 0) break;
                         const double ck = cs[2 * k], sk = cs[2 * k + 1];
-                        lam = qw[r] * (slots[(k - 1) * LQ_SLOT + LQ_X + r] - xr[(k - 1) * 12 + r]) + lq_Atw(ex, r, ck, sk, dt);
+                        lam = slots[(k - 1) * LQ_SLOT + LQ_X + r] + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
                         LMPC_SYNC();
                     }
                 }
@@ -1023,37 +1088,46 @@ __global__ void __launch_bounds__(64, LS == 1 ? 2 : 1) lmpc_lq_kernel(const DevP
     LQ_STAMP_FLUSH(qp);
 }
 
-#define LMPC_LQ_INST(LS_, T_)                                                                                    \
-    template __global__ void lmpc_lq_kernel<LS_, T_>(const DevParams, const double*, const uint8_t*, const double*, \
+#define LMPC_LQ_INST(LS_, T_, W_)                                                                                    \
+    template __global__ void lmpc_lq_kernel<LS_, T_, W_>(const DevParams, const double*, const uint8_t*, const double*, \
                                                      int, double*, int32_t*, int32_t*, const uint8_t*);
-LMPC_LQ_INST(1, false)
-LMPC_LQ_INST(2, false)
-LMPC_LQ_INST(1, true)
-LMPC_LQ_INST(2, true)
+LMPC_LQ_INST(1, false, 1)
+LMPC_LQ_INST(1, false, 2)
+LMPC_LQ_INST(2, false, 1)
+LMPC_LQ_INST(1, true, 1)
+LMPC_LQ_INST(1, true, 2)
+LMPC_LQ_INST(2, true, 1)
 #undef LMPC_LQ_INST
 
-template <int LS, bool TERRAIN>
+template <int LS, bool TERRAIN, int WPE>
 static void launch_lq_variant(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                               int batch, double* grf, int32_t* status, int32_t* iters, const uint8_t* done,
                               hipStream_t stream) {
     const size_t lds = lq_lds_bytes(prm.H);
-    (void)hipFuncSetAttribute((const void*)lmpc_lq_kernel<LS, TERRAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    hipLaunchKernelGGL((lmpc_lq_kernel<LS, TERRAIN>), dim3(batch), dim3(LMPC_WAVE), lds, stream, prm, rec, contact,
-                       normals, batch, grf, status, iters, done);
+    (void)hipFuncSetAttribute((const void*)lmpc_lq_kernel<LS, TERRAIN, WPE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((lmpc_lq_kernel<LS, TERRAIN, WPE>), dim3(batch), dim3(LMPC_WAVE), lds, stream, prm, rec,
+                       contact, normals, batch, grf, status, iters, done);
 }
 
-// Host-side launcher (lmpc_capi.cpp): cold solves of every QP the dense kernel did not take.
+// Host-side launcher (lmpc_capi.cpp): cold solves of every QP the dense kernel did not take.  Two waves per SIMD
+// only where the batch has more QPs than the device has SIMDs and more than four fit a CU's LDS (up to one QP per
+// SIMD the lone-wave instance, free of spills, is faster, and the two-wave one would let the dispatcher stack two
+// QPs on one SIMD while others idle).  Same arithmetic: the choice never changes a result bit.
 hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals, int batch,
                      double* grf, int32_t* status, int32_t* iters, const uint8_t* done, hipStream_t stream) {
     const bool two = 4 * prm.H > 64;
+    const bool w2 = !two && 5 * lq_lds_bytes(prm.H) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
+#define LMPC_LQ_LAUNCH(LS_, T_, W_) \
+    launch_lq_variant<LS_, T_, W_>(prm, rec, contact, normals, batch, grf, status, iters, done, stream)
     if (normals) {
-        if (two) launch_lq_variant<2, true>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
-        else launch_lq_variant<1, true>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
+        if (two) LMPC_LQ_LAUNCH(2, true, 1);
+        else w2 ? LMPC_LQ_LAUNCH(1, true, 2) : LMPC_LQ_LAUNCH(1, true, 1);
     } else {
-        if (two) launch_lq_variant<2, false>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
-        else launch_lq_variant<1, false>(prm, rec, contact, normals, batch, grf, status, iters, done, stream);
+        if (two) LMPC_LQ_LAUNCH(2, false, 1);
+        else w2 ? LMPC_LQ_LAUNCH(1, false, 2) : LMPC_LQ_LAUNCH(1, false, 1);
     }
+#undef LMPC_LQ_LAUNCH
     return hipGetLastError();
 }
 

@@ -32,6 +32,12 @@ from oracle import oracle as O  # noqa: E402
 
 ACT_RATIO = 1e-3
 STEP_FRAC = 0.99
+# RED6=1: the reduced-input form of every Newton system -- the stage's inputs enter the dynamics only through
+# f = Bt u (6 rows), so min_u {1/2 u'Rr u + rr'u : Bt u = f} = 1/2 |v|^2 + const with f = U v - g, W = Bt Rr^-1 Bt' =
+# U U', g = Bt Rr^-1 rr: a Riccati step with 6 inputs of unit cost (two 3x3 pivots whatever the leg count), d' = d - E g
+# and no linear input term; the corrector's new rr enters as rho = dg - K P22 dg (dg = g'' - g').
+RED6 = os.environ.get("RED6", "0") == "1"
+PSD_FLOOR = 1e-10
 
 
 def skew(r):
@@ -73,6 +79,54 @@ def model(p, H, rec, con, normals=None):
 
 
 # ---------------------------------------------------------------------------------------------------------
+def chol_psd(W):
+    """Lower Cholesky factor of a PSD 6x6 with rounding-level pivots (rank-deficient W) floored to zero columns."""
+    n = W.shape[0]
+    L = np.zeros_like(W)
+    for i in range(n):
+        d = W[i, i] - L[i, :i] @ L[i, :i]
+        if not (d > PSD_FLOOR * W[i, i]) or W[i, i] <= 0.0:
+            continue
+        L[i, i] = np.sqrt(d)
+        for r in range(i + 1, n):
+            L[r, i] = (W[r, i] - L[r, :i] @ L[i, :i]) / L[i, i]
+    return L
+
+
+def reduce6(Rr, Bt, rr):
+    """Per stage: U (6x6, W = U U'), g = Bt Rr^-1 rr."""
+    U, g = [], []
+    for k in range(len(Bt)):
+        W = np.zeros((6, 6))
+        gk = np.zeros(6)
+        for j in range(4):
+            Bj = Bt[k][:, 3 * j:3 * j + 3]
+            Ri = np.linalg.inv(Rr[k][j])
+            W += Bj @ Ri @ Bj.T
+            gk += Bj @ (Ri @ rr[k][3 * j:3 * j + 3])
+        U.append(chol_psd(W))
+        g.append(gk)
+    return U, g
+
+
+def p22_of(M, st, k):
+    """P_{k+1}[6:12, 6:12] from Z_k = rows 6-11 of P_{k+1} A_k (A_k's columns 0-5 are unit columns)."""
+    Z = st[k]["Z"][:, :12]
+    dN = M["A"][k][0:6, 6:12]
+    return Z[:, 6:12] - Z[:, 0:6] @ dN
+
+
+def factor6(M, Rr, Bt, rr, dv):
+    """The reduced-input factorisation: factor() on (I, [U | 0], 0, dv - g); returns (stages, g, dv')."""
+    U, g = reduce6(Rr, Bt, rr)
+    H = M["H"]
+    I4 = [[np.eye(3)] * 4 for _ in range(H)]
+    Bp = [np.hstack([U[k], np.zeros((6, 6))]) for k in range(H)]
+    dvp = [dv[k] - g[k] for k in range(H)]
+    st = factor(M, I4, Bp, [np.zeros(12)] * H, dvp, want_S=False)
+    return st, g, dvp
+
+
 def factor(M, Rr, Bt, rr, dv, want_S=True):
     """Rr[k][j] 3x3, Bt[k] 6x12, rr[k] 12, dv[k] 6 -> per-stage (Z 6x13, K, rho, S, v)."""
     H, Q = M["H"], M["Q"]
@@ -243,8 +297,12 @@ def solve(M, tol_mu=1e-4, max_iter=40, max_rounds=8, max_attempts=3):
                   for k in range(H)]
             rr = [np.concatenate([C.T @ (W[k, j] * (s[k, j] - bvec)) if con[k, j] else np.zeros(3)
                                   for j in range(4)]) for k in range(H)]
-            st = factor(M, Rr, Bt_ipm, rr, dv_ipm)
-            xs = forward(M, st, dv_ipm)
+            if RED6:
+                st, g1, dvp = factor6(M, Rr, Bt_ipm, rr, dv_ipm)
+                xs = forward(M, st, dvp)
+            else:
+                st = factor(M, Rr, Bt_ipm, rr, dv_ipm)
+                xs = forward(M, st, dv_ipm)
             ua = costate_u(M, st, xs, Rr, rr, Bt_ipm)
             # predictor step
             dsa = np.zeros_like(s)
@@ -266,9 +324,18 @@ def solve(M, tol_mu=1e-4, max_iter=40, max_rounds=8, max_attempts=3):
             smu = ratio ** 3 * muc
             rr2 = [np.concatenate([C.T @ ((z[k, j] * (s[k, j] - bvec) + smu - dsa[k, j] * dza[k, j]) / s[k, j])
                                    if con[k, j] else np.zeros(3) for j in range(4)]) for k in range(H)]
-            rho_new = [st[k]["S"] @ rr2[k] for k in range(H)]
-            backward_corr(M, st, rho_new)
-            xs = forward(M, st, dv_ipm)
+            if RED6:
+                _, g2 = reduce6(Rr, Bt_ipm, rr2)
+                rho_new = []
+                for k in range(H):
+                    dg = g2[k] - g1[k]
+                    rho_new.append(dg - st[k]["K"] @ (p22_of(M, st, k) @ dg))
+                backward_corr(M, st, rho_new)
+                xs = forward(M, st, dvp)
+            else:
+                rho_new = [st[k]["S"] @ rr2[k] for k in range(H)]
+                backward_corr(M, st, rho_new)
+                xs = forward(M, st, dv_ipm)
             uc = costate_u(M, st, xs, Rr, rr2, Bt_ipm)
             ds = np.zeros_like(s)
             dz = np.zeros_like(z)
@@ -323,8 +390,12 @@ def solve(M, tol_mu=1e-4, max_iter=40, max_rounds=8, max_attempts=3):
             rr.append(np.concatenate(rk))
             Bt.append(B)
             dv.append(d)
-        st = factor(M, Rr, Bt, rr, dv, want_S=False)
-        xs = forward(M, st, dv)
+        if RED6:
+            st, _, dvp = factor6(M, Rr, Bt, rr, dv)
+            xs = forward(M, st, dvp)
+        else:
+            st = factor(M, Rr, Bt, rr, dv, want_S=False)
+            xs = forward(M, st, dv)
         y = costate_u(M, st, xs, Rr, rr, Bt)
         for k in range(H):
             for j in range(4):
