@@ -143,10 +143,11 @@ int lmpc_set_dense_path(lmpc_ctx* ctx, int path);
 int lmpc_get_dense_path(const lmpc_ctx* ctx);
 
 /* Riccati path (ABI 6).  The QPs no dense kernel takes (more than 20 stance leg-steps, H > 16, or a dense QP
- * left without a verified optimum) run on LMPC_RICCATI_LDS (default since round 4: every per-stage factor in
- * LDS, no global workspace) or LMPC_RICCATI_SCRATCH (the round-1..3 kernel: factors in a per-QP global
- * workspace).  Both return the same verified optimum.  Warm-started solves (lmpc_solve_batch_warm) always run
- * on LMPC_RICCATI_SCRATCH.  Fixed per context, never per launch. */
+ * left without a verified optimum) run on LMPC_RICCATI_SCRATCH (the default: factors in a per-QP global
+ * workspace) or LMPC_RICCATI_LDS (round 4: every per-stage factor in LDS, no global workspace, no memory
+ * traffic beyond the record and the forces).  Both return the same verified optimum (DESIGN.md 4d has the
+ * measured trade-off).  Warm-started solves (lmpc_solve_batch_warm) always run on LMPC_RICCATI_SCRATCH.  Fixed
+ * per context, never per launch. */
 #define LMPC_RICCATI_SCRATCH 0
 #define LMPC_RICCATI_LDS 1
 int lmpc_set_riccati_path(lmpc_ctx* ctx, int path);

@@ -115,6 +115,12 @@ __device__ __forceinline__ int lq_opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+// The lane index for the lane-static operand maps of a phase: opaque at two waves per SIMD (recomputed where used:
+// 256 registers cannot hold them across the solve), plain in the lone-wave instance (512 registers: computed once).
+template <int WPE>
+__device__ __forceinline__ int lq_lane(int lane) {
+    return WPE == 1 ? lane : lq_opaque(lane);
+}
 
 // The same products branch-free for a runtime row r: (A x)[r] = x[r] + dt (a1 x[c1] + a2 x[c2]) and
 // (A' w)[r] = w[r] + dt (a1 w[c1] + a2 w[c2]), with lane-static columns and coefficients selected from (cos, sin)
@@ -197,6 +203,9 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     const double* rin = rec + (size_t)qp * RL;
     const double* xr = rin + 33;  // x_ref (global, L2-resident after its first use)
     const double mu = prm.mu, fzmax = prm.fmax, dt = prm.dt;
+    // the serial sweeps load a stage's operands one stage ahead in the lone-wave instance (its latency is
+    // nobody else's to hide); at two waves per SIMD the second set of registers would spill instead
+    constexpr bool LQ_PF = WPE == 1;
     LQ_STAMP_DECL
 
     // ---- prologue: record, terrain frames, I_w^-1, G0, yaw cos / sin ----------------------------------------
@@ -500,24 +509,45 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // Lanes 0-11 hold p (lane r <-> p[r]); y goes through the exchange buffer, t by readlane.
                 {
                     const int r = lane < 12 ? lane : 0;
+                    const int m = lane < 6 ? lane : 0;
+                    // a stage's operands are loaded while the stage before it runs: an LDS load cannot move above
+                    // the fence that orders the exchange buffer, so loaded in the stage itself they would wait a
+                    // round trip on the serial path
+                    struct BwOps {
+                        double v, rho, q, ck, sk, kr[6], zc[6];
+                    };
+                    auto load = [&](int k, BwOps& o) {
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        o.v = sl[LQ_V + r];
+                        o.rho = sl[LQ_RHO + m];
+                        o.q = slots[(k > 0 ? k - 1 : 0) * LQ_SLOT + LQ_X + r];
+                        o.ck = cs[2 * k];
+                        o.sk = cs[2 * k + 1];
+#pragma unroll
+                        for (int n = 0; n < 6; ++n) o.kr[n] = sl[LQ_K + pk6(m, n)];
+#pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) o.zc[mm] = sl[LQ_Z + mm * 13 + r];
+                    };
+                    BwOps cur, nxt;
+                    load(H - 1, cur);
                     double p = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
                     for (int k = H - 1; k >= 0; --k) {
-                        const ldouble* sl = slots + k * LQ_SLOT;
-                        const double y = p + sl[LQ_V + r];
+                        if (!LQ_PF && k < H - 1) load(k, cur);
+                        const double y = p + cur.v;
                         if (lane < 12) ex[r] = y;
                         if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
+                        if (LQ_PF && k > 0) load(k - 1, nxt);
                         LMPC_SYNC();
                         if (k == 0) break;
                         // t_m = sum_n K[m][n] y[6+n] + rho_m, lanes 0-5
-                        const int m = lane < 6 ? lane : 0;
-                        double tv = sl[LQ_RHO + m];
+                        double tv = cur.rho;
 #pragma unroll
-                        for (int n = 0; n < 6; ++n) tv = fma(sl[LQ_K + pk6(m, n)], ex[6 + n], tv);
-                        const double ck = cs[2 * k], sk = cs[2 * k + 1];
-                        double pn = slots[(k - 1) * LQ_SLOT + LQ_X + r] + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
+                        for (int n = 0; n < 6; ++n) tv = fma(cur.kr[n], ex[6 + n], tv);
+                        double pn = cur.q + lq_row_apply(ex, r, lq_atw_row(r, cur.ck, cur.sk), dt);
 #pragma unroll
-                        for (int mm = 0; mm < 6; ++mm) pn = fma(-sl[LQ_Z + mm * 13 + r], readlane_f64(tv, mm), pn);
+                        for (int mm = 0; mm < 6; ++mm) pn = fma(-cur.zc[mm], readlane_f64(tv, mm), pn);
                         p = pn;
+                        if (LQ_PF) cur = nxt;
                         LMPC_SYNC();
                     }
                 }
@@ -531,7 +561,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 const bool want_S = mode == PRED;
                 d4 P;
                 {
-                    const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
+                    const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int r = lr + 4 * i;
@@ -544,7 +574,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // the column 12 of Q^_k (-q x_ref,k-1); out-of-range lanes read the zero words
                 double bg[2], xg[3], qn[3], ckn, skn;
                 auto fetch = [&](int k) {
-                    const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
+                    const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                     const ldouble* sl = slots + k * LQ_SLOT;
                     ckn = cs[2 * k];
                     skn = cs[2 * k + 1];
@@ -571,7 +601,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 };
                 fetch(H - 1);
                 for (int k = H - 1; k >= 0; --k) {
-                    const int fl = lq_opaque(lane), lc = fl & 15, lr = fl >> 4;
+                    const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                     ldouble* sl = slots + k * LQ_SLOT;
                     const double ck = ckn, sk = skn;
                     double bh[2], xb[3], qc[3];
@@ -757,40 +787,56 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
 #endif
             // ======== forward sweep: w = Z x + za ; x' = A x + d - [0; K w + rho] ========
             {
+                struct FwOps {
+                    double kr[6], base, za, z[3], ck, sk;
+                };
+                // lane roles from an opaque lane index (addresses computed per stage, never hoisted at 256 registers);
+                // a stage's operands are loaded while the stage before it runs (see the corrector's backward sweep)
+                auto load = [&](int k, FwOps& o) {
+                    const int ln = lq_lane<WPE>(lane);
+                    const int m = ln < 24 ? (ln >> 2) : 0, part = ln & 3;  // w: lanes 4m..4m+3, 3 terms each
+                    const int r = ln < 12 ? ln : 0;
+                    const int a = r >= 6 ? r - 6 : 0;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+#pragma unroll
+                    for (int mm = 0; mm < 6; ++mm) o.kr[mm] = sl[LQ_K + pk6(a, mm)];
+                    o.base = sl[LQ_DV + a] - sl[LQ_RHO + a];
+                    o.za = sl[LQ_Z + m * 13 + 12];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) o.z[i] = sl[LQ_Z + m * 13 + 3 * part + i];
+                    o.ck = cs[2 * k];
+                    o.sk = cs[2 * k + 1];
+                };
+                FwOps cur, nxt;
+                load(0, cur);
                 if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
                 LMPC_SYNC();
                 for (int k = 0; k < H; ++k) {
-                    // lane roles from an opaque lane index (addresses computed per stage, never hoisted)
-                    const int ln = lq_opaque(lane);
-                    const int m = ln < 24 ? (ln >> 2) : 0, part = ln & 3;  // w: lanes 4m..4m+3, 3 terms each
+                    const int ln = lq_lane<WPE>(lane);
+                    const int part = ln & 3;
                     const int r = ln < 12 ? ln : 0;
-                    const ldouble* sl = slots + k * LQ_SLOT;
                     const ldouble* x = ex + 16;
-                    const int a = r >= 6 ? r - 6 : 0;
-                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
-                    // every operand of the stage is loaded up front; only x waits on the previous stage
-                    double kr[6];
-#pragma unroll
-                    for (int mm = 0; mm < 6; ++mm) kr[mm] = sl[LQ_K + pk6(a, mm)];
-                    const double base = sl[LQ_DV + a] - sl[LQ_RHO + a];
-                    double w = sl[LQ_Z + m * 13 + 3 * part] * x[3 * part];
-                    w = fma(sl[LQ_Z + m * 13 + 3 * part + 1], x[3 * part + 1], w);
-                    w = fma(sl[LQ_Z + m * 13 + 3 * part + 2], x[3 * part + 2], w);
-                    const double xa = lq_row_apply(x, r, lq_ax_row(r, ck, sk), dt);
-                    w = quad_sum(w) + sl[LQ_Z + m * 13 + 12];
+                    if (!LQ_PF && k > 0) load(k, cur);
+                    if (LQ_PF && k + 1 < H) load(k + 1, nxt);
+                    double w = cur.z[0] * x[3 * part];
+                    w = fma(cur.z[1], x[3 * part + 1], w);
+                    w = fma(cur.z[2], x[3 * part + 2], w);
+                    const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
+                    w = quad_sum(w) + cur.za;
                     // w_m to every lane (readlane in uniform control flow: all lanes take part in the DPP sums
                     // above, and the broadcast reads lanes 0, 4, ..., 20)
                     double wb[6];
 #pragma unroll
                     for (int mm = 0; mm < 6; ++mm) wb[mm] = readlane_f64(w, 4 * mm);
                     // K w in two independent halves (a shorter dependent chain)
-                    double k0 = base, k1 = 0.0;
+                    double k0 = cur.base, k1 = 0.0;
 #pragma unroll
                     for (int mm = 0; mm < 3; ++mm) {
-                        k0 = fma(-kr[mm], wb[mm], k0);
-                        k1 = fma(-kr[mm + 3], wb[mm + 3], k1);
+                        k0 = fma(-cur.kr[mm], wb[mm], k0);
+                        k1 = fma(-cur.kr[mm + 3], wb[mm + 3], k1);
                     }
                     const double xn = xa + (r >= 6 ? k0 + k1 : 0.0);
+                    if (LQ_PF) cur = nxt;
                     LMPC_SYNC();
                     if (lane < 12) {
                         ex[16 + r] = xn;
@@ -968,10 +1014,12 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                     for (int k = H - 1; k >= 0; --k) {
                         if (lane < 12) ex[r] = lam;
                         if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_RHO + (lane - 6)] = lam;
+                        // the stage's own operands ahead of the fence (they do not depend on the exchange)
+                        const int kp = k > 0 ? k - 1 : 0;
+                        const double q = slots[kp * LQ_SLOT + LQ_X + r], ck = cs[2 * k], sk = cs[2 * k + 1];
                         LMPC_SYNC();
                         if (k == 0) break;
-                        const double ck = cs[2 * k], sk = cs[2 * k + 1];
-                        lam = slots[(k - 1) * LQ_SLOT + LQ_X + r] + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
+                        lam = q + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
                         LMPC_SYNC();
                     }
                 }
@@ -1117,7 +1165,11 @@ static void launch_lq_variant(const DevParams& prm, const double* rec, const uin
 hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals, int batch,
                      double* grf, int32_t* status, int32_t* iters, const uint8_t* done, hipStream_t stream) {
     const bool two = 4 * prm.H > 64;
+#ifdef LMPC_AB_NO_W2  // diagnostic variant (tools/ab_bench.sh): the lone-wave instance only
+    const bool w2 = false;
+#else
     const bool w2 = !two && 5 * lq_lds_bytes(prm.H) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
+#endif
 #define LMPC_LQ_LAUNCH(LS_, T_, W_) \
     launch_lq_variant<LS_, T_, W_>(prm, rec, contact, normals, batch, grf, status, iters, done, stream)
     if (normals) {

@@ -38,6 +38,7 @@ STEP_FRAC = 0.99
 # and no linear input term; the corrector's new rr enters as rho = dg - K P22 dg (dg = g'' - g').
 RED6 = os.environ.get("RED6", "0") == "1"
 PSD_FLOOR = 1e-10
+RED6_POLISH = os.environ.get("RED6_POLISH", "0") == "1"  # the polish too (loses digits on ill-conditioned W)
 
 
 def skew(r):
@@ -390,7 +391,7 @@ def solve(M, tol_mu=1e-4, max_iter=40, max_rounds=8, max_attempts=3):
             rr.append(np.concatenate(rk))
             Bt.append(B)
             dv.append(d)
-        if RED6:
+        if RED6 and RED6_POLISH:
             st, _, dvp = factor6(M, Rr, Bt, rr, dv)
             xs = forward(M, st, dvp)
         else:
