@@ -1,32 +1,38 @@
 // lmpc_lq.hip -- the Riccati path with every per-stage factor in LDS (gfx950), round 4.
 //
 // One 64-lane wavefront per QP, no global scratch and no outlined calls: the per-stage factors the vector passes
-// need are kept in a 207-double LDS slot per stage (19.7 KB per QP at H = 10, so 8 QPs -- two waves per SIMD --
-// share a CU), and everything else lives in registers.  The QP, the interior point and the polish are those of
-// lmpc_kernels.hip (ConvexQPSolver.cpp:16-346 restated); what changes is how the Newton systems are
-// solved (numpy replica step for step: tools/lq_proto.py):
+// need are kept in a 135-double LDS slot per stage (14.4 KB per QP at H = 10: eight QPs -- two waves per SIMD --
+// share a CU; 36 KB at H = 30: four), and everything else lives in registers.  The QP, the interior point and the
+// polish are those of lmpc_kernels.hip (ConvexQPSolver.cpp:16-346 restated); what changes is how the
+// Newton systems are solved (numpy replica step for step: tools/lq_proto.py, RED6=1):
 //
+//   reduced inputs (interior point): a stage's 12 inputs reach the dynamics only through f = Bt u (rows 6-11), so
+//   min_u {1/2 u'Rr u + rr'u : Bt u = f} = 1/2 |v|^2 + const with f = U v - g, where W = Bt Rr^-1 Bt' = U U' (6 x 6)
+//   and g = Bt Rr^-1 rr: the same value function from a Riccati step with six unit-cost inputs and d' = d - E g --
+//   two 3x3 pivot blocks whatever the number of stance legs, no linear input term.  W_j and g_j come from each leg's
+//   lane (Rr = L L', Y = G0_j L^-T), summed over the stage's quad; U by a 6x6 Cholesky per stage (lane k).  The polish
+//   keeps the full inputs (its per-leg bases T make W ill-conditioned; the polish answer must be exact).
 //   factorisation (stage k = H-1 .. 0), value function of the augmented state [x; 1] in one 16x16 MFMA tile
 //   (P^ = [P p; p' c]: its column 12 is the linear term p, so the backward vector pass of the right-hand side the
 //   factorisation is given comes for free):
-//       C   = P^ B^,  B^ rows 6-11 = [Bt | dv]            -> v = P d (column 12)
-//       Guu = Bt' P22 Bt, + Rr_j at each 3x3 leg pivot (Rr is block diagonal: it enters only its own pivot block)
-//       block Cholesky by legs with L^-1 and X = L^-1 [0 | Bt' | rr] eliminated alongside (as lmpc_kernels.hip)
-//       KH  = X'X                                          -> K = V'V (rows/cols 6-11), rho = Bt Guu^-1 rr (col 12)
-//       S   = X'L^-1 (rows 6-11) = Bt Guu^-1              (interior point only: the corrector's rho = S rr')
+//       C   = P^ B^,  B^ rows 6-11 = [U | 0 | dv'] or [Bt | dv]  -> v = P d (column 12)
+//       Guu = B' P22 B, + I or Rr_j at each 3x3 pivot (block diagonal: it enters only its own pivot block)
+//       block Cholesky with L^-1 and X = L^-1 [0 | B' | r] eliminated alongside (as lmpc_kernels.hip)
+//       KH  = X'X                                          -> K = V'V (rows/cols 6-11), rho = B Guu^-1 r (col 12)
 //       PA  = P^ A^,  A^ = [A d; 0 1]                       -> Z = rows 6-11 of PA (6 x 13; column 12 = za = v2 + p2)
 //       P^_k = Q^_k + A^'PA - M'KH M'  (M' = PA with row 12 = e12), Q^_k column 12 = -Q x_ref,k-1
-//   stored per stage: Z (78), K (21, packed), rho (6), S (72), v (12), x (12), dv (6)
+//   stored per stage: Z (78; before the factorisation U or Bt), K (21, packed), rho (6), v (12), x (12), dv (6)
 //   forward sweep      w = Z x + za ;  x' = A x + d - [0; K w + rho]
 //   inputs (parallel)  from the costate lambda2 = Z A^-1 x' + za - v2 (= P2 x' + p2): u_j = -Rr_j^-1 (rr_j + Bt_j' lambda2)
 //                      (lane-local 3x3 solves: Rr is the leg-step's own input Hessian block)
-//   corrector          rho = S rr' (parallel), then the backward sweep p_k = q_k + A'y - Z'(K za + rho), y = p + v,
-//                      za = y[6:12], then the forward sweep and the inputs as above
+//   corrector          the new rr changes g only: rho = dg - K P22 dg (parallel; P22 recovered from Z), then the
+//                      backward sweep p_k = q_k + A'y - Z'(K za + rho), y = p + v, za = y[6:12], the forward sweep
+//                      and the inputs as above
 //   polish check       the adjoint lambda from the trajectory (independent of the factorisation), as lmpc_kernels.hip
 //
-// The stage-k operands of the factorisation come from LDS (Bt in the S slot, rr in the x slot, dv, written by the
-// leg-step lanes before it) and from the leg-step lanes' registers (Rr_j, by readlane: wave-uniform per stage and leg),
-// fetched one stage ahead.  QPs the condensed dense kernel solved are skipped (its hand-over flags).
+// The stage-k operands of the factorisation come from LDS (U or Bt in the Z field, rr in the x field, dv, written
+// before it) and, in the polish, from the leg-step lanes' registers (Rr_j, by readlane: wave-uniform per stage and
+// leg), fetched one stage ahead.  QPs the condensed dense kernel solved are skipped (its hand-over flags).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -64,14 +70,15 @@ extern "C" int lmpc_debug_lq_dump(double* lds, double* u, double* lds2) {
 
 // ---- LDS layout (doubles) ----------------------------------------------------------------------------------
 // per-stage slot
-constexpr int LQ_Z = 0;      // 78: Z = rows 6-11 of P^_{k+1} A^_k, 6 x 13 row-major (column 12: za = v2 + p2)
+constexpr int LQ_Z = 0;      // 78: Z = rows 6-11 of P^_{k+1} A^_k, 6 x 13 row-major (column 12: za = v2 + p2);
+                             //     before the factorisation its input: U (21, packed lower; interior point) or
+                             //     Bt = G0 T (6 x 12 row-major; polish)
 constexpr int LQ_K = 78;     // 21: K = Bt Guu^-1 Bt', packed lower (pk6)
-constexpr int LQ_RHO = 99;   // 6:  rho = Bt Guu^-1 rr; after the forward sweep lambda2 (inputs / adjoint)
-constexpr int LQ_S = 105;    // 72: S = Bt Guu^-1 (6 x 12); before the factorisation Bt = G0 T (6 x 12)
-constexpr int LQ_V = 177;    // 12: v = P_{k+1} d_k
-constexpr int LQ_X = 189;    // 12: x_{k+1}; before the factorisation rr (the input linear term, 12)
-constexpr int LQ_DV = 201;   // 6:  d_k[6:12] = G0 up - g dt e5
-constexpr int LQ_SLOT = 207;
+constexpr int LQ_RHO = 99;   // 6:  rho; after the forward sweep lambda2 (inputs / adjoint)
+constexpr int LQ_V = 105;    // 12: v = P_{k+1} d_k
+constexpr int LQ_X = 117;    // 12: x_{k+1}; before a polish factorisation rr (the input linear term, 12)
+constexpr int LQ_DV = 129;   // 6:  d_k[6:12] (interior point: less g = Bt Rr^-1 rr)
+constexpr int LQ_SLOT = 135;
 // fixed part
 constexpr int LQF_HDR = 0;     // 40: x0(12) R(9) feet(12)
 constexpr int LQF_G0 = 40;     // 72: B rows 6-11 (terrain: G0 blkdiag(R_j))
@@ -444,27 +451,65 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 cpl[t] = valid[t] && cp;
 #pragma unroll
                 for (int m = 0; m < 6; ++m) du[t][m] = 0.0;
-                if (mode != CORR && valid[t]) {
+                if (mode == POLISH && valid[t]) {
                     ldouble* sl = slots + lsk[t] * LQ_SLOT;
 #pragma unroll
                     for (int m = 0; m < 6; ++m) {
                         const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
 #pragma unroll
-                        for (int a = 0; a < 3; ++a) sl[LQ_S + m * 12 + 3 * j + a] = g0 * T[0 * 3 + a] + g1 * T[1 * 3 + a] + g2 * T[2 * 3 + a];
+                        for (int a = 0; a < 3; ++a) sl[LQ_Z + m * 12 + 3 * j + a] = g0 * T[0 * 3 + a] + g1 * T[1 * 3 + a] + g2 * T[2 * 3 + a];
                         du[t][m] = g0 * up[0] + g1 * up[1] + g2 * up[2];
                     }
 #pragma unroll
                     for (int a = 0; a < 3; ++a) sl[LQ_X + 3 * j + a] = rr[t][a];
                 }
+                if (mode != POLISH) {
+                    // the interior point's Newton systems in reduced inputs (RED6 of tools/lq_proto.py): with
+                    // Rr = L L' (lane-local), Y = G0_j L^-T: the leg's W_j = Y Y' and g_j = Y L^-1 rr (-du, summed
+                    // over the stage's legs below); swing legs add nothing
+                    const double i00 = rsq_nr(Rr[t][0]);
+                    const double l10 = Rr[t][1] * i00, l20 = Rr[t][2] * i00;
+                    const double i11 = rsq_nr(fma(-l10, l10, Rr[t][3]));
+                    const double l21 = fma(-l20, l10, Rr[t][4]) * i11;
+                    const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, Rr[t][5])));
+                    const double m10 = -l10 * i00 * i11, m21 = -l21 * i11 * i22, m20 = fma(l10 * l21, i11, -l20) * i00 * i22;
+                    const double c0 = rr[t][0] * i00;                               // L^-1 rr
+                    const double c1 = fma(m10, rr[t][0], i11 * rr[t][1]);
+                    const double c2 = fma(m20, rr[t][0], fma(m21, rr[t][1], i22 * rr[t][2]));
+                    double Y[6][3];
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) {
+                        const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
+                        Y[m][0] = st[t] ? g0 * i00 : 0.0;
+                        Y[m][1] = st[t] ? fma(g0, m10, g1 * i11) : 0.0;
+                        Y[m][2] = st[t] ? fma(g0, m20, fma(g1, m21, g2 * i22)) : 0.0;
+                        du[t][m] = -fma(Y[m][0], c0, fma(Y[m][1], c1, Y[m][2] * c2));
+                    }
+                    if (mode == PRED) {  // W_k = sum over the quad, entry by entry, to the Z field (U's place)
+                        ldouble* wz = slots + lsk[t] * LQ_SLOT + LQ_Z;
+                        const bool lead = valid[t] && j == 0;
+#pragma unroll
+                        for (int m = 0; m < 6; ++m)
+#pragma unroll
+                            for (int n = 0; n <= m; ++n) {
+                                const double w = quad_sum(fma(Y[m][0], Y[n][0], fma(Y[m][1], Y[n][1], Y[m][2] * Y[n][2])));
+                                if (lead) wz[pk6(m, n)] = w;
+                            }
+                    }
+                }
             }
-            // dv_k = sum over the stage's legs of G0_j up - g dt e5 (lanes 4k..4k+3 of a stage: a quad)
-            if (mode != CORR) {
+            // per stage, summed over its legs (lanes 4k..4k+3: a quad): polish dv_k = sum_j G0_j up_j - g dt e5; interior
+            // point dv_k - g_k (predictor) and W_k, the corrector's dg = g'' - g' (to the rho slot)
 #pragma unroll
-                for (int t = 0; t < LS; ++t) {
+            for (int t = 0; t < LS; ++t) {
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) du[t][m] = quad_sum(du[t][m]);
-                    if (valid[t] && lsj[t] == 0) {
-                        ldouble* sl = slots + lsk[t] * LQ_SLOT;
+                for (int m = 0; m < 6; ++m) du[t][m] = quad_sum(du[t][m]);
+                if (valid[t] && lsj[t] == 0) {
+                    ldouble* sl = slots + lsk[t] * LQ_SLOT;
+                    if (mode == CORR) {
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) sl[LQ_RHO + m] = -du[t][m] + sl[LQ_DV + m] + (m == 5 ? prm.grav * dt : 0.0);
+                    } else {
 #pragma unroll
                         for (int m = 0; m < 6; ++m) sl[LQ_DV + m] = du[t][m] - (m == 5 ? prm.grav * dt : 0.0);
                     }
@@ -486,23 +531,39 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
             LQ_STAMP(1);  // leg-step work
 
             if (mode == CORR) {
-                // ======== corrector: rho = S rr' (per stage, quad-reduced), then the backward sweep ========
+                // ======== corrector: rho = dg - K P22 dg per stage (the new rr enters through g only), then the
+                // backward sweep.  P22 = P_{k+1}[6:12, 6:12] from Z_k = rows 6-11 of P_{k+1} A_k (A_k's columns 0-5
+                // are unit columns): P22 = Z[:, 6:12] - Z[:, 0:6] dtN[0:6, 6:12].  h = P22 dg goes to Z's column 12
+                // (za, rewritten by the sweep), then rho over dg in the rho slot ========
+                constexpr int NT6 = (6 * LMPC_MAX_HORIZON + 63) / 64;
 #pragma unroll
-                for (int t = 0; t < LS; ++t) {
-                    double pr[6];
-                    const int j = lsj[t];
-                    const ldouble* sl = slots + lsk[t] * LQ_SLOT;
+                for (int i = 0; i < NT6; ++i) {
+                    if (64 * i >= 6 * H) break;  // wave-uniform
+                    const int e = lane + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
+                    const int k = ec / 6, m = ec - 6 * k;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+                    const double dtc = dt * cs[2 * k], dts = dt * cs[2 * k + 1];
+                    const ldouble* dg = sl + LQ_RHO;
+                    const ldouble* zr = sl + LQ_Z + m * 13;
+                    const double e0 = fma(dtc, dg[0], dts * dg[1]), e1 = fma(dtc, dg[1], -dts * dg[0]);
+                    double h = -fma(zr[0], e0, zr[1] * e1);
 #pragma unroll
-                    for (int m = 0; m < 6; ++m)
-                        pr[m] = sl[LQ_S + m * 12 + 3 * j] * rr[t][0] + sl[LQ_S + m * 12 + 3 * j + 1] * rr[t][1] +
-                                sl[LQ_S + m * 12 + 3 * j + 2] * rr[t][2];
+                    for (int n = 2; n < 6; ++n) h = fma(-zr[n], dt * dg[n], h);
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) pr[m] = quad_sum(pr[m]);
-                    if (valid[t] && j == 0) {
-                        ldouble* so_ = slots + lsk[t] * LQ_SLOT;
+                    for (int n = 0; n < 6; ++n) h = fma(zr[6 + n], dg[n], h);
+                    if (e < 6 * H) slots[k * LQ_SLOT + LQ_Z + m * 13 + 12] = h;
+                }
+                LMPC_SYNC();
 #pragma unroll
-                        for (int m = 0; m < 6; ++m) so_[LQ_RHO + m] = pr[m];
-                    }
+                for (int i = 0; i < NT6; ++i) {
+                    if (64 * i >= 6 * H) break;  // wave-uniform
+                    const int e = lane + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
+                    const int k = ec / 6, m = ec - 6 * k;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+                    double rho = sl[LQ_RHO + m];
+#pragma unroll
+                    for (int n = 0; n < 6; ++n) rho = fma(-sl[LQ_K + pk6(m, n)], sl[LQ_Z + n * 13 + 12], rho);
+                    if (e < 6 * H) slots[k * LQ_SLOT + LQ_RHO + m] = rho;  // only this lane reads this dg
                 }
                 LMPC_SYNC();
                 // backward: y = p_{k+1} + v_k, za = y[6:12] -> Z column 12, t = K za + rho, p_k = q_k + A'y - Z't.
@@ -558,7 +619,39 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // (integer work off the critical path): held across the loop -- or hoisted out of the solve loop by
                 // loop-invariant code motion -- they would stay live through every other phase and push the kernel's
                 // long-lived state past the 256 registers of two waves per SIMD.
-                const bool want_S = mode == PRED;
+                // interior point: reduced inputs -- B^ rows 6-11 = [U | 0 | dv'], unit input Hessian, X = L^-1 [0 | U' | 0],
+                // two 3x3 pivot blocks whatever the stage's leg count; polish: Bt, Rr_j, rr as staged by the legs
+                const bool red = mode != POLISH;
+                if (red) {
+                    // U_k = chol(W_k) for every stage at once (lane k), in place of W in the Z field; pivots at rounding
+                    // level (W is rank-deficient with fewer than two stance legs) leave a zero column
+                    for (int k = lane; k < H; k += 64) {
+                        ldouble* wz = slots + k * LQ_SLOT + LQ_Z;
+                        double w[21];
+#pragma unroll
+                        for (int e = 0; e < 21; ++e) w[e] = wz[e];
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) {
+                            const double wd = w[pk6(c, c)];
+                            double d = wd;
+#pragma unroll
+                            for (int b = 0; b < c; ++b) d = fma(-w[pk6(c, b)], w[pk6(c, b)], d);
+                            const bool ok = d > 1e-10 * wd && wd > 0.0;
+                            const double inv = ok ? rsq_nr(d) : 0.0;
+                            w[pk6(c, c)] = ok ? d * inv : 0.0;
+#pragma unroll
+                            for (int r2 = c + 1; r2 < 6; ++r2) {
+                                double v = w[pk6(r2, c)];
+#pragma unroll
+                                for (int b = 0; b < c; ++b) v = fma(-w[pk6(r2, b)], w[pk6(c, b)], v);
+                                w[pk6(r2, c)] = v * inv;
+                            }
+                        }
+#pragma unroll
+                        for (int e = 0; e < 21; ++e) wz[e] = w[e];
+                    }
+                    LMPC_SYNC();
+                }
                 d4 P;
                 {
                     const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
@@ -581,15 +674,19 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
 #pragma unroll
                     for (int kk = 0; kk < 2; ++kk) {
                         const int r = 4 * (kk + 1) + lr;
-                        const bool in = r >= 6 && r < 12 && lc <= 12;
-                        const int off = lc < 12 ? LQ_S + (r - 6) * 12 + lc : LQ_DV + (r - 6);
+                        const int a = r - 6;
+                        // reduced: U[a][lc] (lower: lc <= a); polish: Bt[a][lc]; column 12: dv
+                        const bool in = r >= 6 && r < 12 && (lc == 12 || (red ? lc <= a : lc < 12));
+                        const int off = lc == 12 ? LQ_DV + a : (red ? LQ_Z + pk6(a, lc) : LQ_Z + a * 12 + lc);
                         bg[kk] = (in ? sl : zero)[in ? off : 0];
                     }
 #pragma unroll
                     for (int i = 0; i < 3; ++i) {
                         const int r = lr + 4 * i;
-                        const bool in = lc >= 6 && lc <= 12;
-                        const int off = lc < 12 ? LQ_S + (lc - 6) * 12 + r : LQ_X + r;
+                        const int a = lc - 6;
+                        // X columns 6-11: reduced U[a][r] (r <= a), polish Bt[a][r]; column 12: rr (polish only)
+                        const bool in = lc >= 6 && (red ? (lc < 12 && r <= a) : lc <= 12);
+                        const int off = lc == 12 ? LQ_X + r : (red ? LQ_Z + pk6(a, r) : LQ_Z + a * 12 + r);
                         xg[i] = (in ? sl : zero)[in ? off : 0];
                     }
                     const int km = k > 0 ? k - 1 : 0;
@@ -654,7 +751,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         X[i] = (i < 3) ? xb[i < 3 ? i : 0] : 0.0;
                     }
                     const int ls0 = 4 * k;
-                    const int amask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
+                    const int lmask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
+                    const int amask = red ? (lmask ? 3 : 0) : lmask;
 #pragma unroll
                     for (int blk = 0; blk < 4; ++blk) {
                         if (!((amask >> blk) & 1)) continue;
@@ -665,8 +763,13 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         // Rr_j of this leg-step, from its lane (wave-uniform)
                         const int srcl = (ls0 + blk) & 63, srct = (ls0 + blk) >> 6;
                         double Rj[6];
+                        if (red) {  // unit input Hessian (wave-uniform branch)
 #pragma unroll
-                        for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
+                            for (int e = 0; e < 6; ++e) Rj[e] = (e == 0 || e == 3 || e == 5) ? 1.0 : 0.0;
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
+                        }
                         // the three tiles' pivot rows through LDS in one round trip (the fence ahead orders the
                         // previous block's reads of the staging rows before these writes)
                         LMPC_SYNC();
@@ -761,18 +864,6 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         P = Pn;
                     }
                     LQ_STAMP(14);  // factorisation: KZ, P
-                    if (want_S) {  // S = X'L^-1 rows 6-11 = Bt Guu^-1 (off the critical path)
-                        d4 SS = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                        for (int kk = 0; kk < 3; ++kk) SS = MFMA64(X[kk], Li[kk], SS);
-#pragma unroll
-                        for (int i = 1; i < 3; ++i) {
-                            const int r = lr + 4 * i;
-                            const bool so = r >= 6 && r < 12 && lc < 12;
-                            (so ? sl : sink)[so ? LQ_S + (r - 6) * 12 + lc : lane] = SS[i];
-                        }
-                    }
-                    LQ_STAMP(15);  // factorisation: S
                     // the pivot staging and the next stage's slot reads are ordered by the next LMPC_SYNC
                 }
                 LMPC_SYNC();
