@@ -41,8 +41,8 @@ def parse():
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
                     help="dense-path kernel (lmpc_set_dense_path); default ipm")
-    ap.add_argument("--riccati", choices=["lds", "scratch"], default="scratch",
-                    help="Riccati kernel of the QPs no dense kernel takes (lmpc_set_riccati_path); default scratch")
+    ap.add_argument("--riccati", choices=["lds", "scratch"], default="lds",
+                    help="Riccati kernel of the QPs no dense kernel takes (lmpc_set_riccati_path); default lds")
     ap.add_argument("--index-offset", type=int, default=0,
                     help="shift the global instance indices (robustness checks on other samples; recorded in config)")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",

@@ -143,18 +143,19 @@ int lmpc_set_dense_path(lmpc_ctx* ctx, int path);
 int lmpc_get_dense_path(const lmpc_ctx* ctx);
 
 /* Riccati path (ABI 6).  The QPs no dense kernel takes (more than 20 stance leg-steps, H > 16, or a dense QP
- * left without a verified optimum) run on LMPC_RICCATI_SCRATCH (the default: factors in a per-QP global
- * workspace) or LMPC_RICCATI_LDS (round 4: every per-stage factor in LDS, no global workspace, no memory
- * traffic beyond the record and the forces).  Both return the same verified optimum (DESIGN.md 4d has the
- * measured trade-off).  Warm-started solves (lmpc_solve_batch_warm) always run on LMPC_RICCATI_SCRATCH.  Fixed
+ * left without a verified optimum) run on LMPC_RICCATI_LDS (the default since round 4: every per-stage factor
+ * in LDS, no global workspace, the interior point's Newton systems in reduced inputs) or LMPC_RICCATI_SCRATCH (the
+ * round-1..3 kernel: factors in a per-QP global workspace).  Both return the same verified optimum (DESIGN.md 4d
+ * has the measurements).  Warm-started solves (lmpc_solve_batch_warm) always run on LMPC_RICCATI_SCRATCH.  Fixed
  * per context, never per launch. */
 #define LMPC_RICCATI_SCRATCH 0
 #define LMPC_RICCATI_LDS 1
 int lmpc_set_riccati_path(lmpc_ctx* ctx, int path);
 int lmpc_get_riccati_path(const lmpc_ctx* ctx);
 
-/* Pre-allocates the per-QP factor workspace for batches up to `batch` (the
- * device path grows it on demand; call this before capturing a HIP graph). */
+/* Pre-allocates the per-QP device workspace of the context's paths for batches up to `batch`: the dense
+ * path's hand-over flags and, with LMPC_RICCATI_SCRATCH, the factor workspace (the device path grows them on
+ * demand; call this after lmpc_set_riccati_path and before capturing a HIP graph). */
 int lmpc_reserve(lmpc_ctx* ctx, int batch);
 
 /* Host buffers in/out, synchronous.  rec[batch][33+12H], contact[batch][H][4],

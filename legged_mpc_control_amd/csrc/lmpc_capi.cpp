@@ -47,10 +47,11 @@ struct lmpc_ctx {
     uint8_t* d_out = nullptr;
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
-    int riccati = LMPC_RICCATI_SCRATCH;  // the Riccati kernel of cold solves (lmpc_set_riccati_path)
+    int riccati = LMPC_RICCATI_LDS;  // the Riccati kernel of cold solves (lmpc_set_riccati_path)
     double* d_scratch = nullptr;  // per-QP Riccati factors (L^-1, V, K, P2) of the scratch kernel, grown on demand
     uint8_t* d_done = nullptr;    // per-QP flag: solved by the dense-path kernel (else the Riccati kernel solves it)
     size_t scratch_qps = 0;
+    size_t done_qps = 0;
     double* d_crec = nullptr;     // records expanded from commands (lmpc_solve_commands_device), grown on demand
     uint8_t* d_ccon = nullptr;
     size_t cmd_qps = 0;
@@ -156,6 +157,7 @@ void free_bufs(lmpc_ctx* c) {
     c->d_scratch = nullptr;
     c->d_done = nullptr;
     c->scratch_qps = 0;
+    c->done_qps = 0;
     (void)hipFree(c->d_crec);
     (void)hipFree(c->d_ccon);
     c->d_crec = nullptr;
@@ -164,13 +166,51 @@ void free_bufs(lmpc_ctx* c) {
     c->d_in = c->d_out = c->h_in = c->h_out = nullptr;
 }
 
+// The per-QP device buffers of a batch: the dense path's hand-over flags (always) and, when the scratch Riccati
+// kernel runs (selected, or a warm start), its factor workspace.  Grown, never shrunk; a buffer in use by a queued
+// launch is waited for before it is freed.
+int ensure_ws(lmpc_ctx* c, int batch, bool scratch) {
+    const bool grow_done = (size_t)batch > c->done_qps, grow_scr = scratch && (size_t)batch > c->scratch_qps;
+    if (!grow_done && !grow_scr) return LMPC_OK;
+    DeviceScope ds(c->device);
+    if (!ds.ok) return LMPC_ERR_DEVICE;
+    if (c->d_done || c->d_scratch) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipDeviceSynchronize();  // queued launches on callers' streams may still read the old buffers
+    }
+    if (grow_done) {
+        (void)hipFree(c->d_done);
+        c->d_done = nullptr;
+        c->done_qps = 0;
+        if (hipMalloc(&c->d_done, (size_t)batch) != hipSuccess) {
+            c->d_done = nullptr;
+            return LMPC_ERR_ALLOC;
+        }
+        c->done_qps = (size_t)batch;
+    }
+    if (grow_scr) {
+        (void)hipFree(c->d_scratch);
+        c->d_scratch = nullptr;
+        c->scratch_qps = 0;
+        if (hipMalloc(&c->d_scratch, (size_t)batch * lmpc::scratch_doubles_per_qp(c->H) * sizeof(double)) != hipSuccess) {
+            c->d_scratch = nullptr;
+            return LMPC_ERR_ALLOC;
+        }
+        c->scratch_qps = (size_t)batch;
+    }
+    return LMPC_OK;
+}
+
 // The Riccati kernel of a cold solve: the LDS-resident one (lmpc_lq.hip) or the scratch one (lmpc_kernels.hip,
-// which needs the per-QP global workspace, grown by lmpc_reserve).
+// which needs the per-QP global workspace).
+bool uses_scratch(const lmpc_ctx* c, const lmpc::DevParams& prm) {
+    return c->riccati != LMPC_RICCATI_LDS || prm.warm_act || prm.act_out;
+}
+
 hipError_t launch_riccati(const lmpc_ctx* c, const lmpc::DevParams& prm, const double* rec, const uint8_t* con,
                           const double* nrm, int batch, double* grf, int32_t* st, int32_t* it, const uint8_t* done,
                           hipStream_t s) {
-    if (c->riccati == LMPC_RICCATI_LDS && !prm.warm_act && !prm.act_out)
-        return lmpc::launch_lq(prm, rec, con, nrm, batch, grf, st, it, done, s);
+    if (!uses_scratch(c, prm)) return lmpc::launch_lq(prm, rec, con, nrm, batch, grf, st, it, done, s);
     return lmpc::launch_qp(prm, rec, con, nrm, batch, grf, st, it, c->d_scratch, done, s);
 }
 
@@ -224,7 +264,7 @@ int lmpc_create(const lmpc_params* p, int horizon, int max_batch, int device, lm
             return LMPC_ERR_ALLOC;
         }
     }
-    if (max_batch > 0 && lmpc_reserve(c, max_batch) != LMPC_OK) {
+    if (max_batch > 0 && ensure_ws(c, max_batch, c->riccati == LMPC_RICCATI_SCRATCH) != LMPC_OK) {
         free_bufs(c);
         (void)hipEventDestroy(c->ev);
         (void)hipStreamDestroy(c->stream);
@@ -279,27 +319,7 @@ int lmpc_get_riccati_path(const lmpc_ctx* c) { return c ? c->riccati : LMPC_ERR_
 
 int lmpc_reserve(lmpc_ctx* c, int batch) {
     if (!c || batch < 0) return LMPC_ERR_ARG;
-    if ((size_t)batch <= c->scratch_qps) return LMPC_OK;
-    DeviceScope ds(c->device);
-    if (!ds.ok) return LMPC_ERR_DEVICE;
-    if (c->d_scratch) {
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipDeviceSynchronize();  // queued launches on callers' streams may still read the old buffers
-        (void)hipFree(c->d_scratch);
-        (void)hipFree(c->d_done);
-        c->d_scratch = nullptr;
-        c->d_done = nullptr;
-        c->scratch_qps = 0;
-    }
-    if (hipMalloc(&c->d_scratch, (size_t)batch * lmpc::scratch_doubles_per_qp(c->H) * sizeof(double)) != hipSuccess ||
-        hipMalloc(&c->d_done, (size_t)batch) != hipSuccess) {
-        (void)hipFree(c->d_scratch);
-        c->d_scratch = nullptr;
-        c->d_done = nullptr;
-        return LMPC_ERR_ALLOC;
-    }
-    c->scratch_qps = (size_t)batch;
-    return LMPC_OK;
+    return ensure_ws(c, batch, c->riccati == LMPC_RICCATI_SCRATCH);
 }
 
 int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, const double* d_normals,
@@ -310,8 +330,8 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
     if (!ds.ok) return LMPC_ERR_DEVICE;
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (ordered with blocking streams)
     if (!stream_ok(s, c->device)) return LMPC_ERR_ARG;
-    if ((size_t)batch > c->scratch_qps) {
-        const int rc = lmpc_reserve(c, batch);
+    {
+        const int rc = ensure_ws(c, batch, uses_scratch(c, c->prm));
         if (rc != LMPC_OK) return rc;
     }
     hipError_t e = ctx_enter(c, s);
@@ -390,7 +410,7 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
         else ++n_ric;
     }
     const bool gi = prm.dense == 2;
-    if (n_ric && (size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
+    if (n_ric && ensure_ws(c, batch, uses_scratch(c, prm)) != LMPC_OK) return LMPC_ERR_ALLOC;
     hipError_t e = hipSuccess;
     if (n_dense)
         e = gi ? lmpc::launch_gi(prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s)
@@ -411,7 +431,7 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
         bool left = false;
         for (int b = 0; b < batch && !left; ++b) left = hd[b] == 0;
         if (left) {
-            if ((size_t)batch > c->scratch_qps && lmpc_reserve(c, batch) != LMPC_OK) return LMPC_ERR_ALLOC;
+            if (ensure_ws(c, batch, uses_scratch(c, prm)) != LMPC_OK) return LMPC_ERR_ALLOC;
             e = launch_riccati(c, prm, d_rec, d_con, d_nrm, batch, d_grf, d_st, d_st + batch, d_done, s);
             if (e == hipSuccess) e = ctx_leave(c, s);
             if (e != hipSuccess) return launch_rc(e);

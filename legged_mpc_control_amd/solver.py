@@ -69,8 +69,8 @@ class BatchedConvexQPSolver:
     def __init__(self, params: N.LmpcParams, horizon: int, max_batch: int = 1, device: int = 0,
                  options: N.LmpcOptions | None = None, dense_path: str | None = None,
                  riccati_path: str | None = None):
-        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path); riccati_path: "scratch" (default,
-        the global-workspace kernel) or "lds" (the LDS-resident kernel) -- lmpc_set_riccati_path."""
+        """dense_path: "ipm" (default), "gi" or "off" (lmpc_set_dense_path); riccati_path: "lds" (default, the
+        LDS-resident kernel) or "scratch" (the global-workspace kernel) -- lmpc_set_riccati_path."""
         if not (1 <= horizon <= N.LMPC_MAX_HORIZON):
             raise ValueError(f"horizon must be in [1, {N.LMPC_MAX_HORIZON}]")
         self._L = N.lib()

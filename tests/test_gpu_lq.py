@@ -110,14 +110,14 @@ def test_lq_edge_cases_and_status():
 
 
 @pytest.mark.gpu
-def test_lq_device_path_matches_host_path(torch_dev):
-    """The device-pointer entry point gives the host path's bits on the LDS kernel."""
+def test_lq_is_the_default_and_device_path_matches_host_path(torch_dev):
+    """A context runs the LDS kernel unless told otherwise; the device-pointer entry point gives the host path's bits."""
     import torch
 
     from legged_mpc_control_amd import BatchedConvexQPSolver, synth
 
     p, H, rec, con = synth.config_batch(3, count=96, first_index=11)
-    s = BatchedConvexQPSolver(p, H, max_batch=96, riccati_path="lds")
+    s = BatchedConvexQPSolver(p, H, max_batch=96)
     assert s.riccati_path == "lds"
     g, st, _ = s.solve(rec, con)
     d_rec = torch.from_numpy(rec).to(torch_dev)
