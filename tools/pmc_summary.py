@@ -128,7 +128,7 @@ def main():
             "write_bytes": wb,
             "source": f"profiles/{TAG}/pmc_per_dispatch.json",
             "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py "
-                      f"(config {c}, --no-cpu); per-dispatch means of the launch's dense-path kernel + lmpc_qp_kernel; FETCH_SIZE x {read_factor:.3f}, "
+                      f"(config {c}, --no-cpu); per-dispatch means of the launch's dense-path kernel + Riccati kernel (lmpc_lq_kernel by default); FETCH_SIZE x {read_factor:.3f}, "
                       f"WRITE_SIZE x {write_factor:.3f} from profiles/{TAG}/pmc_calibration.json",
         }
     json.dump(per, open(os.path.join(DST, "pmc_per_dispatch.json"), "w"), indent=1)
