@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
             constexpr int NTQ = LS == 1 ? 3 : 6;
             double qxl[NTQ];
 #pragma unroll
-            for (int i = 0; i < NTQ; ++i) qxl[i] = xr[min(lane + 64 * i, 12 * H - 1)];
+            for (int i = 0; i < NTQ; ++i) qxl[i] = xr[min(lq_lane<WPE>(lane) + 64 * i, 12 * H - 1)];
             double du[LS][6];
             bool cpl[LS];
 #pragma unroll
@@ -523,7 +523,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 const int fld = mode == CORR ? LQ_X : LQ_V;
 #pragma unroll
                 for (int i = 0; i < NTQ; ++i) {
-                    const int e = lane + 64 * i, j = e / 12, r = e - 12 * j;
+                    const int e = lq_lane<WPE>(lane) + 64 * i, j = e / 12, r = e - 12 * j;
                     if (e < 12 * H) slots[j * LQ_SLOT + fld + r] = -qw[r] * qxl[i];
                 }
             }
@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
 #pragma unroll
                 for (int i = 0; i < NT6; ++i) {
                     if (64 * i >= 6 * H) break;  // wave-uniform
-                    const int e = lane + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
+                    const int e = lq_lane<WPE>(lane) + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
                     const int k = ec / 6, m = ec - 6 * k;
                     const ldouble* sl = slots + k * LQ_SLOT;
                     const double dtc = dt * cs[2 * k], dts = dt * cs[2 * k + 1];
@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
 #pragma unroll
                 for (int i = 0; i < NT6; ++i) {
                     if (64 * i >= 6 * H) break;  // wave-uniform
-                    const int e = lane + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
+                    const int e = lq_lane<WPE>(lane) + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
                     const int k = ec / 6, m = ec - 6 * k;
                     const ldouble* sl = slots + k * LQ_SLOT;
                     double rho = sl[LQ_RHO + m];
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 if (red) {
                     // U_k = chol(W_k) for every stage at once (lane k), in place of W in the Z field; pivots at rounding
                     // level (W is rank-deficient with fewer than two stance legs) leave a zero column
-                    for (int k = lane; k < H; k += 64) {
+                    for (int k = lq_lane<WPE>(lane); k < H; k += 64) {
                         ldouble* wz = slots + k * LQ_SLOT + LQ_Z;
                         double w[21];
 #pragma unroll
@@ -942,7 +942,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 constexpr int NT6 = (6 * LMPC_MAX_HORIZON + 63) / 64;
 #pragma unroll
                 for (int i = 0; i < NT6; ++i) {
-                    const int e = lane + 64 * i;
+                    const int e = lq_lane<WPE>(lane) + 64 * i;
                     if (64 * i >= 6 * H) break;  // wave-uniform
                     const int ec = e < 6 * H ? e : 6 * H - 1;
                     const int k = ec / 6, m = ec - 6 * k;
@@ -1090,10 +1090,10 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         constexpr int NTQ = LS == 1 ? 3 : 6;
                         double xl[NTQ];
 #pragma unroll
-                        for (int i = 0; i < NTQ; ++i) xl[i] = xr[min(lane + 64 * i, 12 * H - 1)];
+                        for (int i = 0; i < NTQ; ++i) xl[i] = xr[min(lq_lane<WPE>(lane) + 64 * i, 12 * H - 1)];
 #pragma unroll
                         for (int i = 0; i < NTQ; ++i) {
-                            const int e = lane + 64 * i, j = e / 12, rr_ = e - 12 * j;
+                            const int e = lq_lane<WPE>(lane) + 64 * i, j = e / 12, rr_ = e - 12 * j;
                             if (e < 12 * H) {
                                 ldouble* xs = slots + j * LQ_SLOT + LQ_X + rr_;
                                 xs[0] = qw[rr_] * (xs[0] - xl[i]);
