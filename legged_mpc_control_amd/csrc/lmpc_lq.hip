@@ -727,6 +727,17 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                     __builtin_amdgcn_sched_barrier(0);
                     fetch(k > 0 ? k - 1 : 0);
                     __builtin_amdgcn_sched_barrier(0);
+                    // reduced inputs: this lane's U row (c = lc - 6, for its X columns), read before Z_k overwrites U_k
+                    double ur[6];
+                    if (red) {
+                        const bool xc = lc >= 6 && lc < 12;
+                        const int ac = xc ? lc - 6 : 0;
+#pragma unroll
+                        for (int b = 0; b < 6; ++b) {
+                            const bool in = xc && b <= ac;
+                            ur[b] = (in ? sl : zero)[in ? LQ_Z + pk6(ac, b) : 0];
+                        }
+                    }
                     // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
                     if (lc == 12) {
 #pragma unroll
@@ -741,8 +752,56 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : lane] = PA[i];
                     }
                     LQ_STAMP(11);  // factorisation: C, PA, G, Z / v stores
+                    d4 X;
+                    const int ls0 = 4 * k;
+                    const int lmask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
+                    if (red) {
+                        // ---- reduced inputs: Guu' = I + U'P22 U (6 x 6) through LDS once, factored by every lane
+                        // (Guu' >= I: no pivot can fail), X = L^-1 U' (rows 0-5, columns 6-11): each lane solves L y = its U
+                        // row and keeps its own rows of y; a stage without stance legs has U = 0 and X = 0 ----
+                        LMPC_SYNC();  // the previous stage's reads of the staging block come first
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) {
+                            const int r = lr + 4 * i;
+                            if (lc < 6 && r < 6) pv[r * 6 + lc] = G[i];
+                        }
+                        LMPC_SYNC();
+                        double gl[21];
+#pragma unroll
+                        for (int r = 0; r < 6; ++r)
+#pragma unroll
+                            for (int c = 0; c <= r; ++c) gl[pk6(r, c)] = pv[r * 6 + c] + (r == c ? 1.0 : 0.0);
+                        double id[6];
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) {
+                            double d = gl[pk6(c, c)];
+#pragma unroll
+                            for (int b = 0; b < c; ++b) d = fma(-gl[pk6(c, b)], gl[pk6(c, b)], d);
+                            id[c] = rsq_nr(d);
+#pragma unroll
+                            for (int r = c + 1; r < 6; ++r) {
+                                double v = gl[pk6(r, c)];
+#pragma unroll
+                                for (int b = 0; b < c; ++b) v = fma(-gl[pk6(r, b)], gl[pk6(c, b)], v);
+                                gl[pk6(r, c)] = v * id[c];
+                            }
+                        }
+                        // y = L^-1 (this lane's U row): the lane's X column, rows 0-5
+                        double y[6];
+#pragma unroll
+                        for (int r = 0; r < 6; ++r) {
+                            double v = ur[r];
+#pragma unroll
+                            for (int b = 0; b < r; ++b) v = fma(-gl[pk6(r, b)], y[b], v);
+                            y[r] = v * id[r];
+                        }
+                        const bool xc = lc >= 6 && lc < 12 && lmask;
+                        X[0] = xc ? (lr == 0 ? y[0] : lr == 1 ? y[1] : lr == 2 ? y[2] : y[3]) : 0.0;
+                        X[1] = xc && lr < 2 ? (lr == 0 ? y[4] : y[5]) : 0.0;
+                        X[2] = X[3] = 0.0;
+                    } else {
                     // ---- block Cholesky of Guu by legs, L^-1 and X = L^-1 [0 | Bt' | rr] alongside ----
-                    d4 Tg, Li, X;
+                    d4 Tg, Li;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int r = lr + 4 * i;
@@ -750,9 +809,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         Li[i] = (r == lc) ? 1.0 : 0.0;
                         X[i] = (i < 3) ? xb[i < 3 ? i : 0] : 0.0;
                     }
-                    const int ls0 = 4 * k;
-                    const int lmask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
-                    const int amask = red ? (lmask ? 3 : 0) : lmask;
+                    const int amask = lmask;
 #pragma unroll
                     for (int blk = 0; blk < 4; ++blk) {
                         if (!((amask >> blk) & 1)) continue;
@@ -763,13 +820,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         // Rr_j of this leg-step, from its lane (wave-uniform)
                         const int srcl = (ls0 + blk) & 63, srct = (ls0 + blk) >> 6;
                         double Rj[6];
-                        if (red) {  // unit input Hessian (wave-uniform branch)
 #pragma unroll
-                            for (int e = 0; e < 6; ++e) Rj[e] = (e == 0 || e == 3 || e == 5) ? 1.0 : 0.0;
-                        } else {
-#pragma unroll
-                            for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
-                        }
+                        for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
                         // the three tiles' pivot rows through LDS in one round trip (the fence ahead orders the
                         // previous block's reads of the staging rows before these writes)
                         LMPC_SYNC();
@@ -824,6 +876,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         Tg = MFMA64(-av, av, Tg);
                         Li = MFMA64(aw, bw, Li);
                         X = MFMA64(aw, bx, X);
+                    }
                     }
                     LQ_STAMP(12);  // factorisation: leg blocks
                     // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
