@@ -1288,6 +1288,10 @@ LMPC_LQ_INST(1, false, 2)
 LMPC_LQ_INST(2, false, 1)
 LMPC_LQ_INST(1, true, 1)
 LMPC_LQ_INST(1, true, 2)
+#ifdef LMPC_AB_W3  // diagnostic variant: three waves per SIMD (168 registers)
+LMPC_LQ_INST(1, false, 3)
+LMPC_LQ_INST(1, true, 3)
+#endif
 LMPC_LQ_INST(2, true, 1)
 #undef LMPC_LQ_INST
 
@@ -1318,7 +1322,11 @@ hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* con
     launch_lq_variant<LS_, T_, W_>(prm, rec, contact, normals, batch, grf, status, iters, done, stream)
     if (normals) {
         if (two) LMPC_LQ_LAUNCH(2, true, 1);
+#ifdef LMPC_AB_W3
+        else w2 ? LMPC_LQ_LAUNCH(1, true, 3) : LMPC_LQ_LAUNCH(1, true, 1);
+#else
         else w2 ? LMPC_LQ_LAUNCH(1, true, 2) : LMPC_LQ_LAUNCH(1, true, 1);
+#endif
     } else {
         if (two) LMPC_LQ_LAUNCH(2, false, 1);
         else w2 ? LMPC_LQ_LAUNCH(1, false, 2) : LMPC_LQ_LAUNCH(1, false, 1);
