@@ -91,7 +91,14 @@ constexpr int LQF_SINK = 332;  // 64: stores of lanes that hold no pivot row / n
 constexpr int LQF_EX = 396;    // 32: exchange buffer of the serial sweeps
 constexpr int LQF_CS = 428;    // 2H: cos / sin of the reference yaw per step
 constexpr int LQF_FIXED = 428;
-__host__ __device__ constexpr int lq_lds_doubles(int H) { return LQF_FIXED + 2 * H + LQ_SLOT * H; }
+// At H <= LQ_KZ_MAXH (one leg-step per lane) the closed-loop rows KZ = K Z (6 x 12 per stage) are kept too, after the
+// slots: the forward sweep is then one 12-term product per row (x' = A x + dv - KZ x - t, t = K za + rho in the rho
+// field) instead of w = Z x + za followed by K w; eight QPs per CU still fit at H = 10.
+constexpr int LQ_KZ_MAXH = 10;
+__host__ __device__ constexpr bool lq_kzs(int H) { return H <= LQ_KZ_MAXH; }
+__host__ __device__ constexpr int lq_lds_doubles(int H) {
+    return LQF_FIXED + 2 * H + LQ_SLOT * H + (lq_kzs(H) ? 72 * H : 0);
+}
 size_t lq_lds_bytes(int H) { return (size_t)lq_lds_doubles(H) * sizeof(double); }
 
 __device__ __forceinline__ constexpr int pk6(int a, int b) {  // packed lower 6x6, any order
@@ -206,6 +213,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     ldouble* const ex = sm + LQF_EX;
     ldouble* const cs = sm + LQF_CS;
     ldouble* const slots = sm + LQF_FIXED + 2 * H;
+    ldouble* const kzr = slots + LQ_SLOT * H;  // closed-loop rows (kzs only)
+    const bool kzs = LS == 1 && WPE == 2 && lq_kzs(H);  // measured: a gain at two waves per SIMD only
     const int RL = 33 + 12 * H;
     const double* rin = rec + (size_t)qp * RL;
     const double* xr = rin + 33;  // x_ref (global, L2-resident after its first use)
@@ -599,11 +608,13 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
                         if (LQ_PF && k > 0) load(k - 1, nxt);
                         LMPC_SYNC();
-                        if (k == 0) break;
-                        // t_m = sum_n K[m][n] y[6+n] + rho_m, lanes 0-5
+                        // t_m = sum_n K[m][n] y[6+n] + rho_m, lanes 0-5 (with the closed-loop rows it is the forward
+                        // sweep's constant too: stored over rho)
                         double tv = cur.rho;
 #pragma unroll
                         for (int n = 0; n < 6; ++n) tv = fma(cur.kr[n], ex[6 + n], tv);
+                        if (kzs && lane < 6) slots[k * LQ_SLOT + LQ_RHO + lane] = tv;
+                        if (k == 0) break;
                         double pn = cur.q + lq_row_apply(ex, r, lq_atw_row(r, cur.ck, cur.sk), dt);
 #pragma unroll
                         for (int mm = 0; mm < 6; ++mm) pn = fma(-cur.zc[mm], readlane_f64(tv, mm), pn);
@@ -892,16 +903,27 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         (ko ? sl : sink)[ko ? off : lane] = KH[i];
                     }
                     LQ_STAMP(13);  // factorisation: KH, K / rho stores
-                    if (k > 0) {
+                    d4 KZ = {0.0, 0.0, 0.0, 0.0};
+                    if (k > 0 || kzs) {
                         // KZ = KH M' (k-blocks 1-2; M' = PA with row 12 = e12: its k = 12 term is KH column 12 added
                         // to column 12 lane-locally)
-                        d4 KZ = {0.0, 0.0, 0.0, 0.0};
                         KZ = MFMA64(KH[1], PA[1], KZ);
                         KZ = MFMA64(KH[2], PA[2], KZ);
                         if (lc == 12) {
 #pragma unroll
                             for (int i = 0; i < 3; ++i) KZ[i] += KH[i];
                         }
+                        if (kzs) {  // rows 6-11: K Z (columns 0-11) to the KZ region, t = K za + rho (column 12) over rho
+#pragma unroll
+                            for (int i = 1; i < 3; ++i) {
+                                const int r = lr + 4 * i;
+                                const bool zr = r >= 6 && r < 12 && lc <= 12;
+                                ldouble* dst = lc == 12 ? sl + LQ_RHO + (r - 6) : kzr + k * 72 + (r - 6) * 12 + lc;
+                                (zr ? dst : sink + lane)[0] = KZ[i];
+                            }
+                        }
+                    }
+                    if (k > 0) {
                         // P^_k = Q^_k + A^'PA - M'KZ  (rows 0-11; row 12 is never read)
                         d4 Pn;
 #pragma unroll
@@ -930,7 +952,53 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
             }
 #endif
             // ======== forward sweep: w = Z x + za ; x' = A x + d - [0; K w + rho] ========
-            {
+            if (kzs) {
+                // closed-loop rows: x'[6:12] = x[6:12] + dv - t - KZ x (lanes 4a..4a+3: row a, three terms each, a
+                // quad sum), x'[0:6] = (A x)[0:6] on lanes 0-5
+                struct KzOps {
+                    double kz[3], c, ck, sk;
+                };
+                auto load = [&](int k, KzOps& o) {
+                    const int ln = lq_lane<WPE>(lane);
+                    const int a = ln < 24 ? (ln >> 2) : 0, part = ln & 3;
+                    const ldouble* sl = slots + k * LQ_SLOT;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) o.kz[i] = kzr[k * 72 + a * 12 + 3 * part + i];
+                    o.c = sl[LQ_DV + a] - sl[LQ_RHO + a];
+                    o.ck = cs[2 * k];
+                    o.sk = cs[2 * k + 1];
+                };
+                KzOps cur, nxt;
+                load(0, cur);
+                if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
+                LMPC_SYNC();
+                for (int k = 0; k < H; ++k) {
+                    const int ln = lq_lane<WPE>(lane);
+                    const int a = ln < 24 ? (ln >> 2) : 0, part = ln & 3;
+                    const int r = ln < 6 ? ln : 0;
+                    const ldouble* x = ex + 16;
+                    if (!LQ_PF && k > 0) load(k, cur);
+                    if (LQ_PF && k + 1 < H) load(k + 1, nxt);
+                    double w = cur.kz[0] * x[3 * part];
+                    w = fma(cur.kz[1], x[3 * part + 1], w);
+                    w = fma(cur.kz[2], x[3 * part + 2], w);
+                    const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
+                    const double xv = x[6 + a] + cur.c;
+                    w = quad_sum(w);
+                    const double xb = xv - w;
+                    if (LQ_PF) cur = nxt;
+                    LMPC_SYNC();
+                    if (ln < 6) {
+                        ex[16 + r] = xa;
+                        slots[k * LQ_SLOT + LQ_X + r] = xa;
+                    }
+                    if (ln < 24 && part == 0) {
+                        ex[22 + a] = xb;
+                        slots[k * LQ_SLOT + LQ_X + 6 + a] = xb;
+                    }
+                    LMPC_SYNC();
+                }
+            } else {
                 struct FwOps {
                     double kr[6], base, za, z[3], ck, sk;
                 };

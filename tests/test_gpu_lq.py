@@ -64,6 +64,21 @@ def test_lq_live_samples_vs_oracle(cid, count, first):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cid", [2, 4])
+def test_lq_two_wave_instance_vs_oracle(cid):
+    """Batches of more than one QP per SIMD run the two-waves-per-SIMD instance (at H <= 10 with the closed-loop
+    rows in LDS, a different forward-sweep formula): every QP of a 2048-QP batch against the oracle."""
+    from legged_mpc_control_amd import synth
+
+    count = 2048
+    p, H, rec, con = synth.config_batch(cid, count=count, first_index=3 * cid)
+    nrm = synth.config_normals(cid, count, 3 * cid) if cid == 4 else None
+    g, st, _ = _solver(p, H, count).solve(rec, con, normals=nrm)
+    assert (st == 0).all(), np.unique(st, return_counts=True)
+    assert _err(g, _oracle(p, H, rec, con, nrm)) <= TOL
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H", [1, 2, 10, 16, 17, 32])
 def test_lq_horizon_range(H):
     """LS = 1 (H <= 16, two waves per SIMD) and LS = 2 (H > 16) instances, the whole horizon range."""
