@@ -575,6 +575,56 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                     if (e < 6 * H) slots[k * LQ_SLOT + LQ_RHO + m] = rho;  // only this lane reads this dg
                 }
                 LMPC_SYNC();
+                if (kzs) {
+                    // closed-loop rows: p_k = q'_k + A'y - (K Z)'y[6:12] with q'_k = q_k - Z_{k+1}'rho_{k+1} formed for
+                    // every stage first (parallel, into the x field), t = K za + rho afterwards (parallel, over rho)
+                    constexpr int NT12 = (12 * LMPC_MAX_HORIZON + 63) / 64;
+#pragma unroll
+                    for (int i = 0; i < NT12; ++i) {
+                        if (64 * i >= 12 * (H - 1)) break;  // wave-uniform
+                        const int e = lq_lane<WPE>(lane) + 64 * i, ec = e < 12 * (H - 1) ? e : 12 * (H - 1) - 1;
+                        const int k = 1 + ec / 12, r = ec - 12 * (k - 1);
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        double v = slots[(k - 1) * LQ_SLOT + LQ_X + r];
+#pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) v = fma(-sl[LQ_Z + mm * 13 + r], sl[LQ_RHO + mm], v);
+                        if (e < 12 * (H - 1)) slots[(k - 1) * LQ_SLOT + LQ_X + r] = v;
+                    }
+                    LMPC_SYNC();
+                    const int r = lane < 12 ? lane : 0;
+                    double p = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
+                    for (int k = H - 1; k >= 0; --k) {
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        const double y = p + sl[LQ_V + r];
+                        const int kp = k > 0 ? k - 1 : 0;
+                        double kz[6];
+#pragma unroll
+                        for (int a = 0; a < 6; ++a) kz[a] = kzr[k * 72 + a * 12 + r];
+                        const double q = slots[kp * LQ_SLOT + LQ_X + r], ck = cs[2 * k], sk = cs[2 * k + 1];
+                        if (lane < 12) ex[r] = y;
+                        if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
+                        LMPC_SYNC();
+                        if (k == 0) break;
+                        double pn = q + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
+#pragma unroll
+                        for (int a = 0; a < 6; ++a) pn = fma(-kz[a], ex[6 + a], pn);
+                        p = pn;
+                        LMPC_SYNC();
+                    }
+                    LMPC_SYNC();
+                    constexpr int NT6 = (6 * LMPC_MAX_HORIZON + 63) / 64;
+#pragma unroll
+                    for (int i = 0; i < NT6; ++i) {
+                        if (64 * i >= 6 * H) break;  // wave-uniform
+                        const int e = lq_lane<WPE>(lane) + 64 * i, ec = e < 6 * H ? e : 6 * H - 1;
+                        const int k = ec / 6, m = ec - 6 * k;
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        double t = sl[LQ_RHO + m];
+#pragma unroll
+                        for (int n = 0; n < 6; ++n) t = fma(sl[LQ_K + pk6(m, n)], sl[LQ_Z + n * 13 + 12], t);
+                        if (e < 6 * H) slots[k * LQ_SLOT + LQ_RHO + m] = t;  // only this lane reads this rho
+                    }
+                } else
                 // backward: y = p_{k+1} + v_k, za = y[6:12] -> Z column 12, t = K za + rho, p_k = q_k + A'y - Z't.
                 // Lanes 0-11 hold p (lane r <-> p[r]); y goes through the exchange buffer, t by readlane.
                 {
@@ -608,13 +658,11 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
                         if (LQ_PF && k > 0) load(k - 1, nxt);
                         LMPC_SYNC();
-                        // t_m = sum_n K[m][n] y[6+n] + rho_m, lanes 0-5 (with the closed-loop rows it is the forward
-                        // sweep's constant too: stored over rho)
+                        if (k == 0) break;
+                        // t_m = sum_n K[m][n] y[6+n] + rho_m, lanes 0-5
                         double tv = cur.rho;
 #pragma unroll
                         for (int n = 0; n < 6; ++n) tv = fma(cur.kr[n], ex[6 + n], tv);
-                        if (kzs && lane < 6) slots[k * LQ_SLOT + LQ_RHO + lane] = tv;
-                        if (k == 0) break;
                         double pn = cur.q + lq_row_apply(ex, r, lq_atw_row(r, cur.ck, cur.sk), dt);
 #pragma unroll
                         for (int mm = 0; mm < 6; ++mm) pn = fma(-cur.zc[mm], readlane_f64(tv, mm), pn);
