@@ -37,6 +37,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "lmpc/lmpc.h"
 #include "lmpc_device.h"
@@ -724,271 +725,277 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // operands of stage k: B^ k-blocks 1-2 (rows 4+lr, 8+lr: Bt (S slot) in columns 0-11, dv in column
                 // 12), X = [0 | Bt' | rr] (columns 6-11: Bt[lc-6][row], column 12: rr[row] from the x slot), and
                 // the column 12 of Q^_k (-q x_ref,k-1); out-of-range lanes read the zero words
-                double bg[2], xg[3], qn[3], ckn, skn;
-                auto fetch = [&](int k) {
-                    const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
-                    const ldouble* sl = slots + k * LQ_SLOT;
-                    ckn = cs[2 * k];
-                    skn = cs[2 * k + 1];
-#pragma unroll
-                    for (int kk = 0; kk < 2; ++kk) {
-                        const int r = 4 * (kk + 1) + lr;
-                        const int a = r - 6;
-                        // reduced: U[a][lc] (lower: lc <= a); polish: Bt[a][lc]; column 12: dv
-                        const bool in = r >= 6 && r < 12 && (lc == 12 || (red ? lc <= a : lc < 12));
-                        const int off = lc == 12 ? LQ_DV + a : (red ? LQ_Z + pk6(a, lc) : LQ_Z + a * 12 + lc);
-                        bg[kk] = (in ? sl : zero)[in ? off : 0];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const int r = lr + 4 * i;
-                        const int a = lc - 6;
-                        // X columns 6-11: reduced U[a][r] (r <= a), polish Bt[a][r]; column 12: rr (polish only)
-                        const bool in = lc >= 6 && (red ? (lc < 12 && r <= a) : lc <= 12);
-                        const int off = lc == 12 ? LQ_X + r : (red ? LQ_Z + pk6(a, r) : LQ_Z + a * 12 + r);
-                        xg[i] = (in ? sl : zero)[in ? off : 0];
-                    }
-                    const int km = k > 0 ? k - 1 : 0;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const double qv = slots[km * LQ_SLOT + LQ_V + lr + 4 * i];
-                        qn[i] = lc == 12 ? qv : 0.0;
-                    }
-                };
-                fetch(H - 1);
-                for (int k = H - 1; k >= 0; --k) {
-                    const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
-                    ldouble* sl = slots + k * LQ_SLOT;
-                    const double ck = ckn, sk = skn;
-                    double bh[2], xb[3], qc[3];
-#pragma unroll
-                    for (int kk = 0; kk < 2; ++kk) bh[kk] = bg[kk];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        xb[i] = xg[i];
-                        qc[i] = qn[i];
-                    }
-                    // dt N(yaw_k), k-blocks 0-1 (rows 0-7) in the accumulator layout
-                    double nh[2];
-#pragma unroll
-                    for (int kk = 0; kk < 2; ++kk) nh[kk] = lq_dtN(4 * kk + lr, lc, ck, sk, dt);  // selects, no branches
-                    // C = P^ B^ ; PA = P^ A (the d column below) ; Guu = B^' C
-                    d4 C = {0.0, 0.0, 0.0, 0.0};
-                    C = MFMA64(P[1], bh[0], C);
-                    C = MFMA64(P[2], bh[1], C);
-                    d4 PA = P;
-                    PA = MFMA64(P[0], nh[0], PA);
-                    PA = MFMA64(P[1], nh[1], PA);
-                    d4 G = {0.0, 0.0, 0.0, 0.0};
-                    G = MFMA64(bh[0], C[1], G);
-                    G = MFMA64(bh[1], C[2], G);
-                    // next stage's operands, issued while the matrix cores work through the chain above
-                    __builtin_amdgcn_sched_barrier(0);
-                    fetch(k > 0 ? k - 1 : 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    // reduced inputs: this lane's U row (c = lc - 6, for its X columns), read before Z_k overwrites U_k
-                    double ur[6];
-                    if (red) {
-                        const bool xc = lc >= 6 && lc < 12;
-                        const int ac = xc ? lc - 6 : 0;
-#pragma unroll
-                        for (int b = 0; b < 6; ++b) {
-                            const bool in = xc && b <= ac;
-                            ur[b] = (in ? sl : zero)[in ? LQ_Z + pk6(ac, b) : 0];
+                // the stage sweep, specialised for the interior point (reduced inputs) and for the polish
+                auto sweep = [&](auto red_tag) {
+                    constexpr bool red = decltype(red_tag)::value;
+                    double bg[2], xg[3], qn[3], ckn, skn;
+                    auto fetch = [&](int k) {
+                        const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        ckn = cs[2 * k];
+                        skn = cs[2 * k + 1];
+    #pragma unroll
+                        for (int kk = 0; kk < 2; ++kk) {
+                            const int r = 4 * (kk + 1) + lr;
+                            const int a = r - 6;
+                            // reduced: U[a][lc] (lower: lc <= a); polish: Bt[a][lc]; column 12: dv
+                            const bool in = r >= 6 && r < 12 && (lc == 12 || (red ? lc <= a : lc < 12));
+                            const int off = lc == 12 ? LQ_DV + a : (red ? LQ_Z + pk6(a, lc) : LQ_Z + a * 12 + lc);
+                            bg[kk] = (in ? sl : zero)[in ? off : 0];
                         }
-                    }
-                    // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
-                    if (lc == 12) {
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) PA[i] += C[i];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) (lc == 12 ? sl : sink)[lc == 12 ? LQ_V + lr + 4 * i : lane] = C[i];
-#pragma unroll
-                    for (int i = 1; i < 3; ++i) {
-                        const int r = lr + 4 * i;
-                        const bool o = r >= 6 && r < 12 && lc <= 12;
-                        (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : lane] = PA[i];
-                    }
-                    LQ_STAMP(11);  // factorisation: C, PA, G, Z / v stores
-                    d4 X;
-                    const int ls0 = 4 * k;
-                    const int lmask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
-                    if (red) {
-                        // ---- reduced inputs: Guu' = I + U'P22 U (6 x 6) through LDS once, factored by every lane
-                        // (Guu' >= I: no pivot can fail), X = L^-1 U' (rows 0-5, columns 6-11): each lane solves L y = its U
-                        // row and keeps its own rows of y; a stage without stance legs has U = 0 and X = 0 ----
-                        LMPC_SYNC();  // the previous stage's reads of the staging block come first
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) {
+    #pragma unroll
+                        for (int i = 0; i < 3; ++i) {
                             const int r = lr + 4 * i;
-                            if (lc < 6 && r < 6) pv[r * 6 + lc] = G[i];
+                            const int a = lc - 6;
+                            // X columns 6-11: reduced U[a][r] (r <= a), polish Bt[a][r]; column 12: rr (polish only)
+                            const bool in = lc >= 6 && (red ? (lc < 12 && r <= a) : lc <= 12);
+                            const int off = lc == 12 ? LQ_X + r : (red ? LQ_Z + pk6(a, r) : LQ_Z + a * 12 + r);
+                            xg[i] = (in ? sl : zero)[in ? off : 0];
                         }
-                        LMPC_SYNC();
-                        double gl[21];
-#pragma unroll
-                        for (int r = 0; r < 6; ++r)
-#pragma unroll
-                            for (int c = 0; c <= r; ++c) gl[pk6(r, c)] = pv[r * 6 + c] + (r == c ? 1.0 : 0.0);
-                        double id[6];
-#pragma unroll
-                        for (int c = 0; c < 6; ++c) {
-                            double d = gl[pk6(c, c)];
-#pragma unroll
-                            for (int b = 0; b < c; ++b) d = fma(-gl[pk6(c, b)], gl[pk6(c, b)], d);
-                            id[c] = rsq_nr(d);
-#pragma unroll
-                            for (int r = c + 1; r < 6; ++r) {
-                                double v = gl[pk6(r, c)];
-#pragma unroll
-                                for (int b = 0; b < c; ++b) v = fma(-gl[pk6(r, b)], gl[pk6(c, b)], v);
-                                gl[pk6(r, c)] = v * id[c];
+                        const int km = k > 0 ? k - 1 : 0;
+    #pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+                            const double qv = slots[km * LQ_SLOT + LQ_V + lr + 4 * i];
+                            qn[i] = lc == 12 ? qv : 0.0;
+                        }
+                    };
+                    fetch(H - 1);
+                    for (int k = H - 1; k >= 0; --k) {
+                        const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
+                        ldouble* sl = slots + k * LQ_SLOT;
+                        const double ck = ckn, sk = skn;
+                        double bh[2], xb[3], qc[3];
+    #pragma unroll
+                        for (int kk = 0; kk < 2; ++kk) bh[kk] = bg[kk];
+    #pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+                            xb[i] = xg[i];
+                            qc[i] = qn[i];
+                        }
+                        // dt N(yaw_k), k-blocks 0-1 (rows 0-7) in the accumulator layout
+                        double nh[2];
+    #pragma unroll
+                        for (int kk = 0; kk < 2; ++kk) nh[kk] = lq_dtN(4 * kk + lr, lc, ck, sk, dt);  // selects, no branches
+                        // C = P^ B^ ; PA = P^ A (the d column below) ; Guu = B^' C
+                        d4 C = {0.0, 0.0, 0.0, 0.0};
+                        C = MFMA64(P[1], bh[0], C);
+                        C = MFMA64(P[2], bh[1], C);
+                        d4 PA = P;
+                        PA = MFMA64(P[0], nh[0], PA);
+                        PA = MFMA64(P[1], nh[1], PA);
+                        d4 G = {0.0, 0.0, 0.0, 0.0};
+                        G = MFMA64(bh[0], C[1], G);
+                        G = MFMA64(bh[1], C[2], G);
+                        // next stage's operands, issued while the matrix cores work through the chain above
+                        __builtin_amdgcn_sched_barrier(0);
+                        fetch(k > 0 ? k - 1 : 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        // reduced inputs: this lane's U row (c = lc - 6, for its X columns), read before Z_k overwrites U_k
+                        double ur[6];
+                        if (red) {
+                            const bool xc = lc >= 6 && lc < 12;
+                            const int ac = xc ? lc - 6 : 0;
+    #pragma unroll
+                            for (int b = 0; b < 6; ++b) {
+                                const bool in = xc && b <= ac;
+                                ur[b] = (in ? sl : zero)[in ? LQ_Z + pk6(ac, b) : 0];
                             }
                         }
-                        // y = L^-1 (this lane's U row): the lane's X column, rows 0-5
-                        double y[6];
-#pragma unroll
-                        for (int r = 0; r < 6; ++r) {
-                            double v = ur[r];
-#pragma unroll
-                            for (int b = 0; b < r; ++b) v = fma(-gl[pk6(r, b)], y[b], v);
-                            y[r] = v * id[r];
-                        }
-                        const bool xc = lc >= 6 && lc < 12 && lmask;
-                        X[0] = xc ? (lr == 0 ? y[0] : lr == 1 ? y[1] : lr == 2 ? y[2] : y[3]) : 0.0;
-                        X[1] = xc && lr < 2 ? (lr == 0 ? y[4] : y[5]) : 0.0;
-                        X[2] = X[3] = 0.0;
-                    } else {
-                    // ---- block Cholesky of Guu by legs, L^-1 and X = L^-1 [0 | Bt' | rr] alongside ----
-                    d4 Tg, Li;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = lr + 4 * i;
-                        Tg[i] = (r < 12 && lc < 12) ? G[i] : 0.0;
-                        Li[i] = (r == lc) ? 1.0 : 0.0;
-                        X[i] = (i < 3) ? xb[i < 3 ? i : 0] : 0.0;
-                    }
-                    const int amask = lmask;
-#pragma unroll
-                    for (int blk = 0; blk < 4; ++blk) {
-                        if (!((amask >> blk) & 1)) continue;
-                        const int o = 3 * blk;
-                        const int i0 = o >> 2, i1 = (o + 2) >> 2;
-                        const int ra = 4 * i0 + lr - o, rb = 4 * i1 + lr - o;
-                        const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
-                        // Rr_j of this leg-step, from its lane (wave-uniform)
-                        const int srcl = (ls0 + blk) & 63, srct = (ls0 + blk) >> 6;
-                        double Rj[6];
-#pragma unroll
-                        for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
-                        // the three tiles' pivot rows through LDS in one round trip (the fence ahead orders the
-                        // previous block's reads of the staging rows before these writes)
-                        LMPC_SYNC();
-                        {
-                            ldouble* dt0 = ina ? pv + 16 * ra + lc : sink + lane;
-                            dt0[0] = Tg[i0];
-                            if (i1 != i0) {
-                                ldouble* dt1 = inb ? pv + 16 * rb + lc : sink + lane;
-                                dt1[0] = Tg[i1];
-                            }
-                            ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + lane;
-                            da[0] = Li[i0];
-                            ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + lane;
-                            dx[0] = X[i0];
-                            Li[i0] = ina ? 0.0 : Li[i0];
-                            X[i0] = ina ? 0.0 : X[i0];
-                            if (i1 != i0) {
-                                ldouble* db = inb ? pv + 48 + 16 * rb + lc : sink + lane;
-                                db[0] = Li[i1];
-                                ldouble* dy = inb ? pv + 96 + 16 * rb + lc : sink + lane;
-                                dy[0] = X[i1];
-                                Li[i1] = inb ? 0.0 : Li[i1];
-                                X[i1] = inb ? 0.0 : X[i1];
-                            }
-                        }
-                        LMPC_SYNC();
-                        const double p00 = pv[o] + Rj[0], p10 = pv[16 + o] + Rj[1], p11 = pv[16 + o + 1] + Rj[3];
-                        const double p20 = pv[32 + o] + Rj[2], p21 = pv[32 + o + 1] + Rj[4], p22 = pv[32 + o + 2] + Rj[5];
-                        const double t0 = pv[lc], t1 = pv[16 + lc], t2 = pv[32 + lc];
-                        const double w0 = pv[48 + lc], w1 = pv[64 + lc], w2 = pv[80 + lc];
-                        const double y0 = pv[96 + lc], y1 = pv[112 + lc], y2 = pv[128 + lc];
-                        const double i00 = rsq_nr(p00);
-                        const double l10 = p10 * i00, l20 = p20 * i00;
-                        const double i11 = rsq_nr(fma(-l10, l10, p11));
-                        const double l21 = fma(-l20, l10, p21) * i11;
-                        const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
-                        const double x0 = t0 * i00;
-                        const double x1 = fma(-l10, x0, t1) * i11;
-                        const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
-                        const double xs = lr == 0 ? x0 : lr == 1 ? x1 : x2;
-                        const double av = (lc > o + 2 && lc < 12 && lr < 3) ? xs : 0.0;
-                        const double v0 = w0 * i00;
-                        const double v1 = fma(-l10, v0, w1) * i11;
-                        const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
-                        const double q0 = y0 * i00;
-                        const double q1 = fma(-l10, q0, y1) * i11;
-                        const double q2 = fma(-l21, q1, fma(-l20, q0, y2)) * i22;
-                        const double bw = lr == 0 ? v0 : lr == 1 ? v1 : lr == 2 ? v2 : 0.0;
-                        const double bx = lr == 0 ? q0 : lr == 1 ? q1 : lr == 2 ? q2 : 0.0;
-                        const bool cp = lc >= o && lc <= o + 2;
-                        const double aw = cp ? (lr == lc - o ? 1.0 : 0.0) : -av;
-                        Tg = MFMA64(-av, av, Tg);
-                        Li = MFMA64(aw, bw, Li);
-                        X = MFMA64(aw, bx, X);
-                    }
-                    }
-                    LQ_STAMP(12);  // factorisation: leg blocks
-                    // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
-                    d4 KH = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                    for (int kk = 0; kk < 3; ++kk) KH = MFMA64(X[kk], X[kk], KH);
-#pragma unroll
-                    for (int i = 1; i < 3; ++i) {
-                        const int r = lr + 4 * i;
-                        const bool zr = r >= 6 && r < 12;
-                        const bool ko = zr && ((lc >= 6 && lc < 12 && lc <= r) || lc == 12);
-                        const int off = lc == 12 ? LQ_RHO + (r - 6) : LQ_K + pk6(r - 6, lc - 6);
-                        (ko ? sl : sink)[ko ? off : lane] = KH[i];
-                    }
-                    LQ_STAMP(13);  // factorisation: KH, K / rho stores
-                    d4 KZ = {0.0, 0.0, 0.0, 0.0};
-                    if (k > 0 || kzs) {
-                        // KZ = KH M' (k-blocks 1-2; M' = PA with row 12 = e12: its k = 12 term is KH column 12 added
-                        // to column 12 lane-locally)
-                        KZ = MFMA64(KH[1], PA[1], KZ);
-                        KZ = MFMA64(KH[2], PA[2], KZ);
+                        // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
                         if (lc == 12) {
-#pragma unroll
-                            for (int i = 0; i < 3; ++i) KZ[i] += KH[i];
+    #pragma unroll
+                            for (int i = 0; i < 3; ++i) PA[i] += C[i];
                         }
-                        if (kzs) {  // rows 6-11: K Z (columns 0-11) to the KZ region, t = K za + rho (column 12) over rho
-#pragma unroll
-                            for (int i = 1; i < 3; ++i) {
+    #pragma unroll
+                        for (int i = 0; i < 3; ++i) (lc == 12 ? sl : sink)[lc == 12 ? LQ_V + lr + 4 * i : lane] = C[i];
+    #pragma unroll
+                        for (int i = 1; i < 3; ++i) {
+                            const int r = lr + 4 * i;
+                            const bool o = r >= 6 && r < 12 && lc <= 12;
+                            (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : lane] = PA[i];
+                        }
+                        LQ_STAMP(11);  // factorisation: C, PA, G, Z / v stores
+                        d4 X;
+                        const int ls0 = 4 * k;
+                        const int lmask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
+                        if (red) {
+                            // ---- reduced inputs: Guu' = I + U'P22 U (6 x 6) through LDS once, factored by every lane
+                            // (Guu' >= I: no pivot can fail), X = L^-1 U' (rows 0-5, columns 6-11): each lane solves L y = its U
+                            // row and keeps its own rows of y; a stage without stance legs has U = 0 and X = 0 ----
+                            LMPC_SYNC();  // the previous stage's reads of the staging block come first
+    #pragma unroll
+                            for (int i = 0; i < 2; ++i) {
                                 const int r = lr + 4 * i;
-                                const bool zr = r >= 6 && r < 12 && lc <= 12;
-                                ldouble* dst = lc == 12 ? sl + LQ_RHO + (r - 6) : kzr + k * 72 + (r - 6) * 12 + lc;
-                                (zr ? dst : sink + lane)[0] = KZ[i];
+                                if (lc < 6 && r < 6) pv[r * 6 + lc] = G[i];
                             }
-                        }
-                    }
-                    if (k > 0) {
-                        // P^_k = Q^_k + A^'PA - M'KZ  (rows 0-11; row 12 is never read)
-                        d4 Pn;
-#pragma unroll
+                            LMPC_SYNC();
+                            double gl[21];
+    #pragma unroll
+                            for (int r = 0; r < 6; ++r)
+    #pragma unroll
+                                for (int c = 0; c <= r; ++c) gl[pk6(r, c)] = pv[r * 6 + c] + (r == c ? 1.0 : 0.0);
+                            double id[6];
+    #pragma unroll
+                            for (int c = 0; c < 6; ++c) {
+                                double d = gl[pk6(c, c)];
+    #pragma unroll
+                                for (int b = 0; b < c; ++b) d = fma(-gl[pk6(c, b)], gl[pk6(c, b)], d);
+                                id[c] = rsq_nr(d);
+    #pragma unroll
+                                for (int r = c + 1; r < 6; ++r) {
+                                    double v = gl[pk6(r, c)];
+    #pragma unroll
+                                    for (int b = 0; b < c; ++b) v = fma(-gl[pk6(r, b)], gl[pk6(c, b)], v);
+                                    gl[pk6(r, c)] = v * id[c];
+                                }
+                            }
+                            // y = L^-1 (this lane's U row): the lane's X column, rows 0-5
+                            double y[6];
+    #pragma unroll
+                            for (int r = 0; r < 6; ++r) {
+                                double v = ur[r];
+    #pragma unroll
+                                for (int b = 0; b < r; ++b) v = fma(-gl[pk6(r, b)], y[b], v);
+                                y[r] = v * id[r];
+                            }
+                            const bool xc = lc >= 6 && lc < 12 && lmask;
+                            X[0] = xc ? (lr == 0 ? y[0] : lr == 1 ? y[1] : lr == 2 ? y[2] : y[3]) : 0.0;
+                            X[1] = xc && lr < 2 ? (lr == 0 ? y[4] : y[5]) : 0.0;
+                            X[2] = X[3] = 0.0;
+                        } else {
+                        // ---- block Cholesky of Guu by legs, L^-1 and X = L^-1 [0 | Bt' | rr] alongside ----
+                        d4 Tg, Li;
+    #pragma unroll
                         for (int i = 0; i < 4; ++i) {
                             const int r = lr + 4 * i;
-                            const double qd = (r == lc && r < 12) ? qw[r < 12 ? r : 0] : 0.0;
-                            Pn[i] = PA[i] + qd + ((lc == 12 && i < 3) ? qc[i < 3 ? i : 0] : 0.0);
+                            Tg[i] = (r < 12 && lc < 12) ? G[i] : 0.0;
+                            Li[i] = (r == lc) ? 1.0 : 0.0;
+                            X[i] = (i < 3) ? xb[i < 3 ? i : 0] : 0.0;
                         }
-                        Pn = MFMA64(nh[0], PA[0], Pn);
-                        Pn = MFMA64(nh[1], PA[1], Pn);
-                        Pn = MFMA64(-PA[1], KZ[1], Pn);
-                        Pn = MFMA64(-PA[2], KZ[2], Pn);
-                        P = Pn;
+                        const int amask = lmask;
+    #pragma unroll
+                        for (int blk = 0; blk < 4; ++blk) {
+                            if (!((amask >> blk) & 1)) continue;
+                            const int o = 3 * blk;
+                            const int i0 = o >> 2, i1 = (o + 2) >> 2;
+                            const int ra = 4 * i0 + lr - o, rb = 4 * i1 + lr - o;
+                            const bool ina = ra >= 0 && ra < 3, inb = i1 != i0 && rb >= 0 && rb < 3;
+                            // Rr_j of this leg-step, from its lane (wave-uniform)
+                            const int srcl = (ls0 + blk) & 63, srct = (ls0 + blk) >> 6;
+                            double Rj[6];
+    #pragma unroll
+                            for (int e = 0; e < 6; ++e) Rj[e] = readlane_f64(LS == 1 || srct == 0 ? Rr[0][e] : Rr[LS - 1][e], srcl);
+                            // the three tiles' pivot rows through LDS in one round trip (the fence ahead orders the
+                            // previous block's reads of the staging rows before these writes)
+                            LMPC_SYNC();
+                            {
+                                ldouble* dt0 = ina ? pv + 16 * ra + lc : sink + lane;
+                                dt0[0] = Tg[i0];
+                                if (i1 != i0) {
+                                    ldouble* dt1 = inb ? pv + 16 * rb + lc : sink + lane;
+                                    dt1[0] = Tg[i1];
+                                }
+                                ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + lane;
+                                da[0] = Li[i0];
+                                ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + lane;
+                                dx[0] = X[i0];
+                                Li[i0] = ina ? 0.0 : Li[i0];
+                                X[i0] = ina ? 0.0 : X[i0];
+                                if (i1 != i0) {
+                                    ldouble* db = inb ? pv + 48 + 16 * rb + lc : sink + lane;
+                                    db[0] = Li[i1];
+                                    ldouble* dy = inb ? pv + 96 + 16 * rb + lc : sink + lane;
+                                    dy[0] = X[i1];
+                                    Li[i1] = inb ? 0.0 : Li[i1];
+                                    X[i1] = inb ? 0.0 : X[i1];
+                                }
+                            }
+                            LMPC_SYNC();
+                            const double p00 = pv[o] + Rj[0], p10 = pv[16 + o] + Rj[1], p11 = pv[16 + o + 1] + Rj[3];
+                            const double p20 = pv[32 + o] + Rj[2], p21 = pv[32 + o + 1] + Rj[4], p22 = pv[32 + o + 2] + Rj[5];
+                            const double t0 = pv[lc], t1 = pv[16 + lc], t2 = pv[32 + lc];
+                            const double w0 = pv[48 + lc], w1 = pv[64 + lc], w2 = pv[80 + lc];
+                            const double y0 = pv[96 + lc], y1 = pv[112 + lc], y2 = pv[128 + lc];
+                            const double i00 = rsq_nr(p00);
+                            const double l10 = p10 * i00, l20 = p20 * i00;
+                            const double i11 = rsq_nr(fma(-l10, l10, p11));
+                            const double l21 = fma(-l20, l10, p21) * i11;
+                            const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
+                            const double x0 = t0 * i00;
+                            const double x1 = fma(-l10, x0, t1) * i11;
+                            const double x2 = fma(-l21, x1, fma(-l20, x0, t2)) * i22;
+                            const double xs = lr == 0 ? x0 : lr == 1 ? x1 : x2;
+                            const double av = (lc > o + 2 && lc < 12 && lr < 3) ? xs : 0.0;
+                            const double v0 = w0 * i00;
+                            const double v1 = fma(-l10, v0, w1) * i11;
+                            const double v2 = fma(-l21, v1, fma(-l20, v0, w2)) * i22;
+                            const double q0 = y0 * i00;
+                            const double q1 = fma(-l10, q0, y1) * i11;
+                            const double q2 = fma(-l21, q1, fma(-l20, q0, y2)) * i22;
+                            const double bw = lr == 0 ? v0 : lr == 1 ? v1 : lr == 2 ? v2 : 0.0;
+                            const double bx = lr == 0 ? q0 : lr == 1 ? q1 : lr == 2 ? q2 : 0.0;
+                            const bool cp = lc >= o && lc <= o + 2;
+                            const double aw = cp ? (lr == lc - o ? 1.0 : 0.0) : -av;
+                            Tg = MFMA64(-av, av, Tg);
+                            Li = MFMA64(aw, bw, Li);
+                            X = MFMA64(aw, bx, X);
+                        }
+                        }
+                        LQ_STAMP(12);  // factorisation: leg blocks
+                        // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
+                        d4 KH = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll
+                        for (int kk = 0; kk < 3; ++kk) KH = MFMA64(X[kk], X[kk], KH);
+    #pragma unroll
+                        for (int i = 1; i < 3; ++i) {
+                            const int r = lr + 4 * i;
+                            const bool zr = r >= 6 && r < 12;
+                            const bool ko = zr && ((lc >= 6 && lc < 12 && lc <= r) || lc == 12);
+                            const int off = lc == 12 ? LQ_RHO + (r - 6) : LQ_K + pk6(r - 6, lc - 6);
+                            (ko ? sl : sink)[ko ? off : lane] = KH[i];
+                        }
+                        LQ_STAMP(13);  // factorisation: KH, K / rho stores
+                        d4 KZ = {0.0, 0.0, 0.0, 0.0};
+                        if (k > 0 || kzs) {
+                            // KZ = KH M' (k-blocks 1-2; M' = PA with row 12 = e12: its k = 12 term is KH column 12 added
+                            // to column 12 lane-locally)
+                            KZ = MFMA64(KH[1], PA[1], KZ);
+                            KZ = MFMA64(KH[2], PA[2], KZ);
+                            if (lc == 12) {
+    #pragma unroll
+                                for (int i = 0; i < 3; ++i) KZ[i] += KH[i];
+                            }
+                            if (kzs) {  // rows 6-11: K Z (columns 0-11) to the KZ region, t = K za + rho (column 12) over rho
+    #pragma unroll
+                                for (int i = 1; i < 3; ++i) {
+                                    const int r = lr + 4 * i;
+                                    const bool zr = r >= 6 && r < 12 && lc <= 12;
+                                    ldouble* dst = lc == 12 ? sl + LQ_RHO + (r - 6) : kzr + k * 72 + (r - 6) * 12 + lc;
+                                    (zr ? dst : sink + lane)[0] = KZ[i];
+                                }
+                            }
+                        }
+                        if (k > 0) {
+                            // P^_k = Q^_k + A^'PA - M'KZ  (rows 0-11; row 12 is never read)
+                            d4 Pn;
+    #pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int r = lr + 4 * i;
+                                const double qd = (r == lc && r < 12) ? qw[r < 12 ? r : 0] : 0.0;
+                                Pn[i] = PA[i] + qd + ((lc == 12 && i < 3) ? qc[i < 3 ? i : 0] : 0.0);
+                            }
+                            Pn = MFMA64(nh[0], PA[0], Pn);
+                            Pn = MFMA64(nh[1], PA[1], Pn);
+                            Pn = MFMA64(-PA[1], KZ[1], Pn);
+                            Pn = MFMA64(-PA[2], KZ[2], Pn);
+                            P = Pn;
+                        }
+                        LQ_STAMP(14);  // factorisation: KZ, P
+                        // the pivot staging and the next stage's slot reads are ordered by the next LMPC_SYNC
                     }
-                    LQ_STAMP(14);  // factorisation: KZ, P
-                    // the pivot staging and the next stage's slot reads are ordered by the next LMPC_SYNC
-                }
+                };
+                if (mode != POLISH) sweep(std::true_type{});
+                else sweep(std::false_type{});
                 LMPC_SYNC();
                 LQ_STAMP(3);  // factorisation
             }
