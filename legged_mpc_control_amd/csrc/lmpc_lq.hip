@@ -389,154 +389,161 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
             // the tracking terms -Q x_ref,j of every stage, loaded from the record here (global memory: every load
             // issued at once, ahead of the leg-step work) and stored to slot j below -- v field before a
             // factorisation, x field before the corrector's backward sweep -- so the serial sweeps read LDS only
-            constexpr int NTQ = LS == 1 ? 3 : 6;
-            double qxl[NTQ];
-#pragma unroll
-            for (int i = 0; i < NTQ; ++i) qxl[i] = xr[min(lq_lane<WPE>(lane) + 64 * i, 12 * H - 1)];
-            double du[LS][6];
-            bool cpl[LS];
-#pragma unroll
-            for (int t = 0; t < LS; ++t) {
-                const int j = lsj[t];
-                double rb[6];
-                if constexpr (TERRAIN) {
-#pragma unroll
-                    for (int e = 0; e < 6; ++e) rb[e] = rbt[6 * j + e];
-                } else {
-                    rb[0] = prm.r[3 * j]; rb[1] = 0.0; rb[2] = 0.0;
-                    rb[3] = prm.r[3 * j + 1]; rb[4] = 0.0; rb[5] = prm.r[3 * j + 2];
-                }
-                double T[9], up[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-                for (int e = 0; e < 9; ++e) T[e] = (e % 4 == 0 && st[t]) ? 1.0 : 0.0;
-                if (mode == POLISH) {
-                    apex[t] = false;
-                    if (st[t]) apex[t] = leg_basis(act[t], mu, fzmax, T, up);
-                    // Rr = T' Rb T (fixed components -> identity), rr = T' Rb up
-                    const double R3[9] = {rb[0], rb[1], rb[2], rb[1], rb[3], rb[4], rb[2], rb[4], rb[5]};
-                    bool fixed[3];
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) fixed[a] = T[a] == 0.0 && T[3 + a] == 0.0 && T[6 + a] == 0.0;
-                    double RT[9], Ru[3];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-#pragma unroll
-                        for (int b = 0; b < 3; ++b) RT[q * 3 + b] = R3[q * 3 + 0] * T[0 * 3 + b] + R3[q * 3 + 1] * T[1 * 3 + b] + R3[q * 3 + 2] * T[2 * 3 + b];
-                        Ru[q] = R3[q * 3 + 0] * up[0] + R3[q * 3 + 1] * up[1] + R3[q * 3 + 2] * up[2];
-                    }
-                    int e = 0;
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) {
-#pragma unroll
-                        for (int b = a; b < 3; ++b) {
-                            double v = T[0 * 3 + a] * RT[0 * 3 + b] + T[1 * 3 + a] * RT[1 * 3 + b] + T[2 * 3 + a] * RT[2 * 3 + b];
-                            if (fixed[a] || fixed[b]) v = (a == b) ? 1.0 : 0.0;
-                            Rr[t][e++] = v;
-                        }
-                        rr[t][a] = fixed[a] ? 0.0 : T[0 * 3 + a] * Ru[0] + T[1 * 3 + a] * Ru[1] + T[2 * 3 + a] * Ru[2];
-                    }
-                } else if (mode == PRED) {
-                    // interior point: Rr = Rb + C'WC, rr = C'W(s - b) (predictor); identity / zero on swing legs
-                    double W[5] = {0, 0, 0, 0, 0}, wv[5] = {0, 0, 0, 0, 0};
-                    if (st[t]) {
-#pragma unroll
-                        for (int i = 0; i < 5; ++i) {
-                            W[i] = z[t][i] * rcp_nr(s[t][i]);
-                            wv[i] = W[i] * (s[t][i] - (i == 4 ? fzmax : 0.0));
-                        }
-                    }
-                    const double sx = W[0] + W[1], sy = W[2] + W[3];
-                    Rr[t][0] = st[t] ? rb[0] + sx : 1.0;
-                    Rr[t][1] = st[t] ? rb[1] : 0.0;
-                    Rr[t][2] = st[t] ? rb[2] + mu * (W[0] - W[1]) : 0.0;
-                    Rr[t][3] = st[t] ? rb[3] + sy : 1.0;
-                    Rr[t][4] = st[t] ? rb[4] + mu * (W[2] - W[3]) : 0.0;
-                    Rr[t][5] = st[t] ? rb[5] + mu * mu * (sx + sy) + W[4] : 1.0;
-                    cons_tw(wv, mu, rr[t]);
-                }
-                // (CORR: Rr unchanged; rr was set to the corrector's by the predictor step below)
-                bool cp = false;
-#pragma unroll
-                for (int e = 0; e < 9; ++e) cp |= T[e] != 0.0;
-                cpl[t] = valid[t] && cp;
-#pragma unroll
-                for (int m = 0; m < 6; ++m) du[t][m] = 0.0;
-                if (mode == POLISH && valid[t]) {
-                    ldouble* sl = slots + lsk[t] * LQ_SLOT;
-#pragma unroll
-                    for (int m = 0; m < 6; ++m) {
-                        const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
-#pragma unroll
-                        for (int a = 0; a < 3; ++a) sl[LQ_Z + m * 12 + 3 * j + a] = g0 * T[0 * 3 + a] + g1 * T[1 * 3 + a] + g2 * T[2 * 3 + a];
-                        du[t][m] = g0 * up[0] + g1 * up[1] + g2 * up[2];
-                    }
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) sl[LQ_X + 3 * j + a] = rr[t][a];
-                }
-                if (mode != POLISH) {
-                    // the interior point's Newton systems in reduced inputs (RED6 of tools/lq_proto.py): with
-                    // Rr = L L' (lane-local), Y = G0_j L^-T: the leg's W_j = Y Y' and g_j = Y L^-1 rr (-du, summed
-                    // over the stage's legs below); swing legs add nothing
-                    const double i00 = rsq_nr(Rr[t][0]);
-                    const double l10 = Rr[t][1] * i00, l20 = Rr[t][2] * i00;
-                    const double i11 = rsq_nr(fma(-l10, l10, Rr[t][3]));
-                    const double l21 = fma(-l20, l10, Rr[t][4]) * i11;
-                    const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, Rr[t][5])));
-                    const double m10 = -l10 * i00 * i11, m21 = -l21 * i11 * i22, m20 = fma(l10 * l21, i11, -l20) * i00 * i22;
-                    const double c0 = rr[t][0] * i00;                               // L^-1 rr
-                    const double c1 = fma(m10, rr[t][0], i11 * rr[t][1]);
-                    const double c2 = fma(m20, rr[t][0], fma(m21, rr[t][1], i22 * rr[t][2]));
-                    double Y[6][3];
-#pragma unroll
-                    for (int m = 0; m < 6; ++m) {
-                        const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
-                        Y[m][0] = st[t] ? g0 * i00 : 0.0;
-                        Y[m][1] = st[t] ? fma(g0, m10, g1 * i11) : 0.0;
-                        Y[m][2] = st[t] ? fma(g0, m20, fma(g1, m21, g2 * i22)) : 0.0;
-                        du[t][m] = -fma(Y[m][0], c0, fma(Y[m][1], c1, Y[m][2] * c2));
-                    }
-                    if (mode == PRED) {  // W_k = sum over the quad, entry by entry, to the Z field (U's place)
-                        ldouble* wz = slots + lsk[t] * LQ_SLOT + LQ_Z;
-                        const bool lead = valid[t] && j == 0;
-#pragma unroll
-                        for (int m = 0; m < 6; ++m)
-#pragma unroll
-                            for (int n = 0; n <= m; ++n) {
-                                const double w = quad_sum(fma(Y[m][0], Y[n][0], fma(Y[m][1], Y[n][1], Y[m][2] * Y[n][2])));
-                                if (lead) wz[pk6(m, n)] = w;
-                            }
-                    }
-                }
-            }
-            // per stage, summed over its legs (lanes 4k..4k+3: a quad): polish dv_k = sum_j G0_j up_j - g dt e5; interior
-            // point dv_k - g_k (predictor) and W_k, the corrector's dg = g'' - g' (to the rho slot)
-#pragma unroll
-            for (int t = 0; t < LS; ++t) {
-#pragma unroll
-                for (int m = 0; m < 6; ++m) du[t][m] = quad_sum(du[t][m]);
-                if (valid[t] && lsj[t] == 0) {
-                    ldouble* sl = slots + lsk[t] * LQ_SLOT;
-                    if (mode == CORR) {
-#pragma unroll
-                        for (int m = 0; m < 6; ++m) sl[LQ_RHO + m] = -du[t][m] + sl[LQ_DV + m] + (m == 5 ? prm.grav * dt : 0.0);
-                    } else {
-#pragma unroll
-                        for (int m = 0; m < 6; ++m) sl[LQ_DV + m] = du[t][m] - (m == 5 ? prm.grav * dt : 0.0);
-                    }
-                }
-            }
-            // coupled legs per stage (T != 0): ballot, one word per leg-step slot
+            // the leg-step work, specialised per mode at compile time (its three variants share no registers)
             unsigned long long cmask[LS];
-#pragma unroll
-            for (int t = 0; t < LS; ++t) cmask[t] = __ballot(cpl[t]);
-            {
-                const int fld = mode == CORR ? LQ_X : LQ_V;
-#pragma unroll
-                for (int i = 0; i < NTQ; ++i) {
-                    const int e = lq_lane<WPE>(lane) + 64 * i, j = e / 12, r = e - 12 * j;
-                    if (e < 12 * H) slots[j * LQ_SLOT + fld + r] = -qw[r] * qxl[i];
+            auto legwork = [&](auto mode_tag) {
+                constexpr int md = decltype(mode_tag)::value;
+                constexpr int NTQ = LS == 1 ? 3 : 6;
+                double qxl[NTQ];
+    #pragma unroll
+                for (int i = 0; i < NTQ; ++i) qxl[i] = xr[min(lq_lane<WPE>(lane) + 64 * i, 12 * H - 1)];
+                double du[LS][6];
+                bool cpl[LS];
+    #pragma unroll
+                for (int t = 0; t < LS; ++t) {
+                    const int j = lsj[t];
+                    double rb[6];
+                    if constexpr (TERRAIN) {
+    #pragma unroll
+                        for (int e = 0; e < 6; ++e) rb[e] = rbt[6 * j + e];
+                    } else {
+                        rb[0] = prm.r[3 * j]; rb[1] = 0.0; rb[2] = 0.0;
+                        rb[3] = prm.r[3 * j + 1]; rb[4] = 0.0; rb[5] = prm.r[3 * j + 2];
+                    }
+                    double T[9], up[3] = {0.0, 0.0, 0.0};
+    #pragma unroll
+                    for (int e = 0; e < 9; ++e) T[e] = (e % 4 == 0 && st[t]) ? 1.0 : 0.0;
+                    if (md == POLISH) {
+                        apex[t] = false;
+                        if (st[t]) apex[t] = leg_basis(act[t], mu, fzmax, T, up);
+                        // Rr = T' Rb T (fixed components -> identity), rr = T' Rb up
+                        const double R3[9] = {rb[0], rb[1], rb[2], rb[1], rb[3], rb[4], rb[2], rb[4], rb[5]};
+                        bool fixed[3];
+    #pragma unroll
+                        for (int a = 0; a < 3; ++a) fixed[a] = T[a] == 0.0 && T[3 + a] == 0.0 && T[6 + a] == 0.0;
+                        double RT[9], Ru[3];
+    #pragma unroll
+                        for (int q = 0; q < 3; ++q) {
+    #pragma unroll
+                            for (int b = 0; b < 3; ++b) RT[q * 3 + b] = R3[q * 3 + 0] * T[0 * 3 + b] + R3[q * 3 + 1] * T[1 * 3 + b] + R3[q * 3 + 2] * T[2 * 3 + b];
+                            Ru[q] = R3[q * 3 + 0] * up[0] + R3[q * 3 + 1] * up[1] + R3[q * 3 + 2] * up[2];
+                        }
+                        int e = 0;
+    #pragma unroll
+                        for (int a = 0; a < 3; ++a) {
+    #pragma unroll
+                            for (int b = a; b < 3; ++b) {
+                                double v = T[0 * 3 + a] * RT[0 * 3 + b] + T[1 * 3 + a] * RT[1 * 3 + b] + T[2 * 3 + a] * RT[2 * 3 + b];
+                                if (fixed[a] || fixed[b]) v = (a == b) ? 1.0 : 0.0;
+                                Rr[t][e++] = v;
+                            }
+                            rr[t][a] = fixed[a] ? 0.0 : T[0 * 3 + a] * Ru[0] + T[1 * 3 + a] * Ru[1] + T[2 * 3 + a] * Ru[2];
+                        }
+                    } else if (md == PRED) {
+                        // interior point: Rr = Rb + C'WC, rr = C'W(s - b) (predictor); identity / zero on swing legs
+                        double W[5] = {0, 0, 0, 0, 0}, wv[5] = {0, 0, 0, 0, 0};
+                        if (st[t]) {
+    #pragma unroll
+                            for (int i = 0; i < 5; ++i) {
+                                W[i] = z[t][i] * rcp_nr(s[t][i]);
+                                wv[i] = W[i] * (s[t][i] - (i == 4 ? fzmax : 0.0));
+                            }
+                        }
+                        const double sx = W[0] + W[1], sy = W[2] + W[3];
+                        Rr[t][0] = st[t] ? rb[0] + sx : 1.0;
+                        Rr[t][1] = st[t] ? rb[1] : 0.0;
+                        Rr[t][2] = st[t] ? rb[2] + mu * (W[0] - W[1]) : 0.0;
+                        Rr[t][3] = st[t] ? rb[3] + sy : 1.0;
+                        Rr[t][4] = st[t] ? rb[4] + mu * (W[2] - W[3]) : 0.0;
+                        Rr[t][5] = st[t] ? rb[5] + mu * mu * (sx + sy) + W[4] : 1.0;
+                        cons_tw(wv, mu, rr[t]);
+                    }
+                    // (CORR: Rr unchanged; rr was set to the corrector's by the predictor step below)
+                    bool cp = false;
+    #pragma unroll
+                    for (int e = 0; e < 9; ++e) cp |= T[e] != 0.0;
+                    cpl[t] = valid[t] && cp;
+    #pragma unroll
+                    for (int m = 0; m < 6; ++m) du[t][m] = 0.0;
+                    if (md == POLISH && valid[t]) {
+                        ldouble* sl = slots + lsk[t] * LQ_SLOT;
+    #pragma unroll
+                        for (int m = 0; m < 6; ++m) {
+                            const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
+    #pragma unroll
+                            for (int a = 0; a < 3; ++a) sl[LQ_Z + m * 12 + 3 * j + a] = g0 * T[0 * 3 + a] + g1 * T[1 * 3 + a] + g2 * T[2 * 3 + a];
+                            du[t][m] = g0 * up[0] + g1 * up[1] + g2 * up[2];
+                        }
+    #pragma unroll
+                        for (int a = 0; a < 3; ++a) sl[LQ_X + 3 * j + a] = rr[t][a];
+                    }
+                    if (md != POLISH) {
+                        // the interior point's Newton systems in reduced inputs (RED6 of tools/lq_proto.py): with
+                        // Rr = L L' (lane-local), Y = G0_j L^-T: the leg's W_j = Y Y' and g_j = Y L^-1 rr (-du, summed
+                        // over the stage's legs below); swing legs add nothing
+                        const double i00 = rsq_nr(Rr[t][0]);
+                        const double l10 = Rr[t][1] * i00, l20 = Rr[t][2] * i00;
+                        const double i11 = rsq_nr(fma(-l10, l10, Rr[t][3]));
+                        const double l21 = fma(-l20, l10, Rr[t][4]) * i11;
+                        const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, Rr[t][5])));
+                        const double m10 = -l10 * i00 * i11, m21 = -l21 * i11 * i22, m20 = fma(l10 * l21, i11, -l20) * i00 * i22;
+                        const double c0 = rr[t][0] * i00;                               // L^-1 rr
+                        const double c1 = fma(m10, rr[t][0], i11 * rr[t][1]);
+                        const double c2 = fma(m20, rr[t][0], fma(m21, rr[t][1], i22 * rr[t][2]));
+                        double Y[6][3];
+    #pragma unroll
+                        for (int m = 0; m < 6; ++m) {
+                            const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
+                            Y[m][0] = st[t] ? g0 * i00 : 0.0;
+                            Y[m][1] = st[t] ? fma(g0, m10, g1 * i11) : 0.0;
+                            Y[m][2] = st[t] ? fma(g0, m20, fma(g1, m21, g2 * i22)) : 0.0;
+                            du[t][m] = -fma(Y[m][0], c0, fma(Y[m][1], c1, Y[m][2] * c2));
+                        }
+                        if (md == PRED) {  // W_k = sum over the quad, entry by entry, to the Z field (U's place)
+                            ldouble* wz = slots + lsk[t] * LQ_SLOT + LQ_Z;
+                            const bool lead = valid[t] && j == 0;
+    #pragma unroll
+                            for (int m = 0; m < 6; ++m)
+    #pragma unroll
+                                for (int n = 0; n <= m; ++n) {
+                                    const double w = quad_sum(fma(Y[m][0], Y[n][0], fma(Y[m][1], Y[n][1], Y[m][2] * Y[n][2])));
+                                    if (lead) wz[pk6(m, n)] = w;
+                                }
+                        }
+                    }
                 }
-            }
+                // per stage, summed over its legs (lanes 4k..4k+3: a quad): polish dv_k = sum_j G0_j up_j - g dt e5; interior
+                // point dv_k - g_k (predictor) and W_k, the corrector's dg = g'' - g' (to the rho slot)
+    #pragma unroll
+                for (int t = 0; t < LS; ++t) {
+    #pragma unroll
+                    for (int m = 0; m < 6; ++m) du[t][m] = quad_sum(du[t][m]);
+                    if (valid[t] && lsj[t] == 0) {
+                        ldouble* sl = slots + lsk[t] * LQ_SLOT;
+                        if (md == CORR) {
+    #pragma unroll
+                            for (int m = 0; m < 6; ++m) sl[LQ_RHO + m] = -du[t][m] + sl[LQ_DV + m] + (m == 5 ? prm.grav * dt : 0.0);
+                        } else {
+    #pragma unroll
+                            for (int m = 0; m < 6; ++m) sl[LQ_DV + m] = du[t][m] - (m == 5 ? prm.grav * dt : 0.0);
+                        }
+                    }
+                }
+                // coupled legs per stage (T != 0): ballot, one word per leg-step slot
+    #pragma unroll
+                for (int t = 0; t < LS; ++t) cmask[t] = __ballot(cpl[t]);
+                {
+                    const int fld = md == CORR ? LQ_X : LQ_V;
+    #pragma unroll
+                    for (int i = 0; i < NTQ; ++i) {
+                        const int e = lq_lane<WPE>(lane) + 64 * i, j = e / 12, r = e - 12 * j;
+                        if (e < 12 * H) slots[j * LQ_SLOT + fld + r] = -qw[r] * qxl[i];
+                    }
+                }
+            };
+            if (mode == PRED) legwork(std::integral_constant<int, PRED>{});
+            else if (mode == CORR) legwork(std::integral_constant<int, CORR>{});
+            else legwork(std::integral_constant<int, POLISH>{});
             LMPC_SYNC();
             LQ_STAMP(1);  // leg-step work
 
