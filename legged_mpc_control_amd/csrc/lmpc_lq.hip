@@ -1013,159 +1013,166 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 for (int e = lane; e < lq_lds_doubles(H) && e < 8192; e += 64) lmpc_lq_dbg2[e] = sm[e];
             }
 #endif
-            // ======== forward sweep: w = Z x + za ; x' = A x + d - [0; K w + rho] ========
-            if (kzs) {
-                // closed-loop rows: x'[6:12] = x[6:12] + dv - t - KZ x (lanes 4a..4a+3: row a, three terms each, a
-                // quad sum), x'[0:6] = (A x)[0:6] on lanes 0-5
-                struct KzOps {
-                    double kz[3], c, ck, sk;
-                };
-                auto load = [&](int k, KzOps& o) {
-                    const int ln = lq_lane<WPE>(lane);
-                    const int a = ln < 24 ? (ln >> 2) : 0, part = ln & 3;
-                    const ldouble* sl = slots + k * LQ_SLOT;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) o.kz[i] = kzr[k * 72 + a * 12 + 3 * part + i];
-                    o.c = sl[LQ_DV + a] - sl[LQ_RHO + a];
-                    o.ck = cs[2 * k];
-                    o.sk = cs[2 * k + 1];
-                };
-                KzOps cur, nxt;
-                load(0, cur);
-                if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
-                LMPC_SYNC();
-                for (int k = 0; k < H; ++k) {
-                    const int ln = lq_lane<WPE>(lane);
-                    const int a = ln < 24 ? (ln >> 2) : 0, part = ln & 3;
-                    const int r = ln < 6 ? ln : 0;
-                    const ldouble* x = ex + 16;
-                    if (!LQ_PF && k > 0) load(k, cur);
-                    if (LQ_PF && k + 1 < H) load(k + 1, nxt);
-                    double w = cur.kz[0] * x[3 * part];
-                    w = fma(cur.kz[1], x[3 * part + 1], w);
-                    w = fma(cur.kz[2], x[3 * part + 2], w);
-                    const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
-                    const double xv = x[6 + a] + cur.c;
-                    w = quad_sum(w);
-                    const double xb = xv - w;
-                    if (LQ_PF) cur = nxt;
+            // the forward sweep and the inputs, specialised per mode (the polish recomputes each leg's basis)
+            auto fwd_inputs = [&](auto mode_tag) {
+                constexpr int md = decltype(mode_tag)::value;
+                (void)md;
+                // ======== forward sweep: w = Z x + za ; x' = A x + d - [0; K w + rho] ========
+                if (kzs) {
+                    // closed-loop rows: x'[6:12] = x[6:12] + dv - t - KZ x (lanes 4a..4a+3: row a, three terms each, a
+                    // quad sum), x'[0:6] = (A x)[0:6] on lanes 0-5
+                    struct KzOps {
+                        double kz[3], c, ck, sk;
+                    };
+                    auto load = [&](int k, KzOps& o) {
+                        const int ln = lq_lane<WPE>(lane);
+                        const int a = ln < 24 ? (ln >> 2) : 0, part = ln & 3;
+                        const ldouble* sl = slots + k * LQ_SLOT;
+    #pragma unroll
+                        for (int i = 0; i < 3; ++i) o.kz[i] = kzr[k * 72 + a * 12 + 3 * part + i];
+                        o.c = sl[LQ_DV + a] - sl[LQ_RHO + a];
+                        o.ck = cs[2 * k];
+                        o.sk = cs[2 * k + 1];
+                    };
+                    KzOps cur, nxt;
+                    load(0, cur);
+                    if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
                     LMPC_SYNC();
-                    if (ln < 6) {
-                        ex[16 + r] = xa;
-                        slots[k * LQ_SLOT + LQ_X + r] = xa;
+                    for (int k = 0; k < H; ++k) {
+                        const int ln = lq_lane<WPE>(lane);
+                        const int a = ln < 24 ? (ln >> 2) : 0, part = ln & 3;
+                        const int r = ln < 6 ? ln : 0;
+                        const ldouble* x = ex + 16;
+                        if (!LQ_PF && k > 0) load(k, cur);
+                        if (LQ_PF && k + 1 < H) load(k + 1, nxt);
+                        double w = cur.kz[0] * x[3 * part];
+                        w = fma(cur.kz[1], x[3 * part + 1], w);
+                        w = fma(cur.kz[2], x[3 * part + 2], w);
+                        const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
+                        const double xv = x[6 + a] + cur.c;
+                        w = quad_sum(w);
+                        const double xb = xv - w;
+                        if (LQ_PF) cur = nxt;
+                        LMPC_SYNC();
+                        if (ln < 6) {
+                            ex[16 + r] = xa;
+                            slots[k * LQ_SLOT + LQ_X + r] = xa;
+                        }
+                        if (ln < 24 && part == 0) {
+                            ex[22 + a] = xb;
+                            slots[k * LQ_SLOT + LQ_X + 6 + a] = xb;
+                        }
+                        LMPC_SYNC();
                     }
-                    if (ln < 24 && part == 0) {
-                        ex[22 + a] = xb;
-                        slots[k * LQ_SLOT + LQ_X + 6 + a] = xb;
+                } else {
+                    struct FwOps {
+                        double kr[6], base, za, z[3], ck, sk;
+                    };
+                    // lane roles from an opaque lane index (addresses computed per stage, never hoisted at 256 registers);
+                    // a stage's operands are loaded while the stage before it runs (see the corrector's backward sweep)
+                    auto load = [&](int k, FwOps& o) {
+                        const int ln = lq_lane<WPE>(lane);
+                        const int m = ln < 24 ? (ln >> 2) : 0, part = ln & 3;  // w: lanes 4m..4m+3, 3 terms each
+                        const int r = ln < 12 ? ln : 0;
+                        const int a = r >= 6 ? r - 6 : 0;
+                        const ldouble* sl = slots + k * LQ_SLOT;
+    #pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) o.kr[mm] = sl[LQ_K + pk6(a, mm)];
+                        o.base = sl[LQ_DV + a] - sl[LQ_RHO + a];
+                        o.za = sl[LQ_Z + m * 13 + 12];
+    #pragma unroll
+                        for (int i = 0; i < 3; ++i) o.z[i] = sl[LQ_Z + m * 13 + 3 * part + i];
+                        o.ck = cs[2 * k];
+                        o.sk = cs[2 * k + 1];
+                    };
+                    FwOps cur, nxt;
+                    load(0, cur);
+                    if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
+                    LMPC_SYNC();
+                    for (int k = 0; k < H; ++k) {
+                        const int ln = lq_lane<WPE>(lane);
+                        const int part = ln & 3;
+                        const int r = ln < 12 ? ln : 0;
+                        const ldouble* x = ex + 16;
+                        if (!LQ_PF && k > 0) load(k, cur);
+                        if (LQ_PF && k + 1 < H) load(k + 1, nxt);
+                        double w = cur.z[0] * x[3 * part];
+                        w = fma(cur.z[1], x[3 * part + 1], w);
+                        w = fma(cur.z[2], x[3 * part + 2], w);
+                        const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
+                        w = quad_sum(w) + cur.za;
+                        // w_m to every lane (readlane in uniform control flow: all lanes take part in the DPP sums
+                        // above, and the broadcast reads lanes 0, 4, ..., 20)
+                        double wb[6];
+    #pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) wb[mm] = readlane_f64(w, 4 * mm);
+                        // K w in two independent halves (a shorter dependent chain)
+                        double k0 = cur.base, k1 = 0.0;
+    #pragma unroll
+                        for (int mm = 0; mm < 3; ++mm) {
+                            k0 = fma(-cur.kr[mm], wb[mm], k0);
+                            k1 = fma(-cur.kr[mm + 3], wb[mm + 3], k1);
+                        }
+                        const double xn = xa + (r >= 6 ? k0 + k1 : 0.0);
+                        if (LQ_PF) cur = nxt;
+                        LMPC_SYNC();
+                        if (lane < 12) {
+                            ex[16 + r] = xn;
+                            slots[k * LQ_SLOT + LQ_X + r] = xn;
+                        }
+                        LMPC_SYNC();
+                    }
+                }
+                LQ_STAMP(4);  // forward sweep
+                // ======== inputs from the costate: lambda2 = Z A^-1 x' + za - v2 (-> rho slot), then per leg-step ========
+                {
+                    constexpr int NT6 = (6 * LMPC_MAX_HORIZON + 63) / 64;
+    #pragma unroll
+                    for (int i = 0; i < NT6; ++i) {
+                        const int e = lq_lane<WPE>(lane) + 64 * i;
+                        if (64 * i >= 6 * H) break;  // wave-uniform
+                        const int ec = e < 6 * H ? e : 6 * H - 1;
+                        const int k = ec / 6, m = ec - 6 * k;
+                        const ldouble* sl = slots + k * LQ_SLOT;
+                        const ldouble* xk = sl + LQ_X;
+                        const double ck = cs[2 * k], sk = cs[2 * k + 1];
+                        double lam = sl[LQ_Z + m * 13 + 12] - sl[LQ_V + 6 + m];
+    #pragma unroll
+                        for (int c = 0; c < 12; ++c) lam = fma(sl[LQ_Z + m * 13 + c], lq_Ax(xk, c, ck, sk, dt, -1.0), lam);
+                        if (e < 6 * H) slots[k * LQ_SLOT + LQ_RHO + m] = lam;
                     }
                     LMPC_SYNC();
-                }
-            } else {
-                struct FwOps {
-                    double kr[6], base, za, z[3], ck, sk;
-                };
-                // lane roles from an opaque lane index (addresses computed per stage, never hoisted at 256 registers);
-                // a stage's operands are loaded while the stage before it runs (see the corrector's backward sweep)
-                auto load = [&](int k, FwOps& o) {
-                    const int ln = lq_lane<WPE>(lane);
-                    const int m = ln < 24 ? (ln >> 2) : 0, part = ln & 3;  // w: lanes 4m..4m+3, 3 terms each
-                    const int r = ln < 12 ? ln : 0;
-                    const int a = r >= 6 ? r - 6 : 0;
-                    const ldouble* sl = slots + k * LQ_SLOT;
-#pragma unroll
-                    for (int mm = 0; mm < 6; ++mm) o.kr[mm] = sl[LQ_K + pk6(a, mm)];
-                    o.base = sl[LQ_DV + a] - sl[LQ_RHO + a];
-                    o.za = sl[LQ_Z + m * 13 + 12];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) o.z[i] = sl[LQ_Z + m * 13 + 3 * part + i];
-                    o.ck = cs[2 * k];
-                    o.sk = cs[2 * k + 1];
-                };
-                FwOps cur, nxt;
-                load(0, cur);
-                if (lane < 12) ex[16 + lane] = hdr[lane];  // x0
-                LMPC_SYNC();
-                for (int k = 0; k < H; ++k) {
-                    const int ln = lq_lane<WPE>(lane);
-                    const int part = ln & 3;
-                    const int r = ln < 12 ? ln : 0;
-                    const ldouble* x = ex + 16;
-                    if (!LQ_PF && k > 0) load(k, cur);
-                    if (LQ_PF && k + 1 < H) load(k + 1, nxt);
-                    double w = cur.z[0] * x[3 * part];
-                    w = fma(cur.z[1], x[3 * part + 1], w);
-                    w = fma(cur.z[2], x[3 * part + 2], w);
-                    const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
-                    w = quad_sum(w) + cur.za;
-                    // w_m to every lane (readlane in uniform control flow: all lanes take part in the DPP sums
-                    // above, and the broadcast reads lanes 0, 4, ..., 20)
-                    double wb[6];
-#pragma unroll
-                    for (int mm = 0; mm < 6; ++mm) wb[mm] = readlane_f64(w, 4 * mm);
-                    // K w in two independent halves (a shorter dependent chain)
-                    double k0 = cur.base, k1 = 0.0;
-#pragma unroll
-                    for (int mm = 0; mm < 3; ++mm) {
-                        k0 = fma(-cur.kr[mm], wb[mm], k0);
-                        k1 = fma(-cur.kr[mm + 3], wb[mm + 3], k1);
+    #pragma unroll
+                    for (int t = 0; t < LS; ++t) {
+                        u[t][0] = u[t][1] = u[t][2] = 0.0;
+                        if (!st[t]) continue;
+                        const int j = lsj[t];
+                        const ldouble* lam = slots + lsk[t] * LQ_SLOT + LQ_RHO;
+                        double l2[6];
+    #pragma unroll
+                        for (int mm = 0; mm < 6; ++mm) l2[mm] = lam[mm];
+                        // b = rr + T' G0_j' lambda2 ; y = -Rr^-1 b ; u = up + T y
+                        double gj[3], b[3], y[3];
+    #pragma unroll
+                        for (int p = 0; p < 3; ++p) {
+                            double v = 0.0;
+    #pragma unroll
+                            for (int mm = 0; mm < 6; ++mm) v = fma(G0s[mm * 12 + 3 * j + p], l2[mm], v);
+                            gj[p] = v;
+                        }
+                        double T[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, up[3] = {0.0, 0.0, 0.0};
+                        if (md == POLISH) (void)leg_basis(act[t], mu, fzmax, T, up);
+    #pragma unroll
+                        for (int a = 0; a < 3; ++a) b[a] = -(rr[t][a] + T[0 * 3 + a] * gj[0] + T[1 * 3 + a] * gj[1] + T[2 * 3 + a] * gj[2]);
+                        sym3_solve(Rr[t], b, y);
+    #pragma unroll
+                        for (int p = 0; p < 3; ++p) u[t][p] = up[p] + T[p * 3] * y[0] + T[p * 3 + 1] * y[1] + T[p * 3 + 2] * y[2];
                     }
-                    const double xn = xa + (r >= 6 ? k0 + k1 : 0.0);
-                    if (LQ_PF) cur = nxt;
-                    LMPC_SYNC();
-                    if (lane < 12) {
-                        ex[16 + r] = xn;
-                        slots[k * LQ_SLOT + LQ_X + r] = xn;
-                    }
-                    LMPC_SYNC();
                 }
-            }
-            LQ_STAMP(4);  // forward sweep
-            // ======== inputs from the costate: lambda2 = Z A^-1 x' + za - v2 (-> rho slot), then per leg-step ========
-            {
-                constexpr int NT6 = (6 * LMPC_MAX_HORIZON + 63) / 64;
-#pragma unroll
-                for (int i = 0; i < NT6; ++i) {
-                    const int e = lq_lane<WPE>(lane) + 64 * i;
-                    if (64 * i >= 6 * H) break;  // wave-uniform
-                    const int ec = e < 6 * H ? e : 6 * H - 1;
-                    const int k = ec / 6, m = ec - 6 * k;
-                    const ldouble* sl = slots + k * LQ_SLOT;
-                    const ldouble* xk = sl + LQ_X;
-                    const double ck = cs[2 * k], sk = cs[2 * k + 1];
-                    double lam = sl[LQ_Z + m * 13 + 12] - sl[LQ_V + 6 + m];
-#pragma unroll
-                    for (int c = 0; c < 12; ++c) lam = fma(sl[LQ_Z + m * 13 + c], lq_Ax(xk, c, ck, sk, dt, -1.0), lam);
-                    if (e < 6 * H) slots[k * LQ_SLOT + LQ_RHO + m] = lam;
-                }
-                LMPC_SYNC();
-#pragma unroll
-                for (int t = 0; t < LS; ++t) {
-                    u[t][0] = u[t][1] = u[t][2] = 0.0;
-                    if (!st[t]) continue;
-                    const int j = lsj[t];
-                    const ldouble* lam = slots + lsk[t] * LQ_SLOT + LQ_RHO;
-                    double l2[6];
-#pragma unroll
-                    for (int mm = 0; mm < 6; ++mm) l2[mm] = lam[mm];
-                    // b = rr + T' G0_j' lambda2 ; y = -Rr^-1 b ; u = up + T y
-                    double gj[3], b[3], y[3];
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int mm = 0; mm < 6; ++mm) v = fma(G0s[mm * 12 + 3 * j + p], l2[mm], v);
-                        gj[p] = v;
-                    }
-                    double T[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, up[3] = {0.0, 0.0, 0.0};
-                    if (mode == POLISH) (void)leg_basis(act[t], mu, fzmax, T, up);
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) b[a] = -(rr[t][a] + T[0 * 3 + a] * gj[0] + T[1 * 3 + a] * gj[1] + T[2 * 3 + a] * gj[2]);
-                    sym3_solve(Rr[t], b, y);
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) u[t][p] = up[p] + T[p * 3] * y[0] + T[p * 3 + 1] * y[1] + T[p * 3 + 2] * y[2];
-                }
-            }
-            LQ_STAMP(5);  // inputs
+                LQ_STAMP(5);  // inputs
+            };
+            if (mode == POLISH) fwd_inputs(std::integral_constant<int, POLISH>{});
+            else fwd_inputs(std::integral_constant<int, PRED>{});
 #ifdef LMPC_LQ_DEBUG
             // diagnostic build only: QP 0's LDS and inputs after the first predictor solve (tools/lq_debug.py)
             if (qp == 0 && mode == PRED && ipm_it == 0) {
