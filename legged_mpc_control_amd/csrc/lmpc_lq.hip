@@ -52,7 +52,11 @@ __device__ unsigned long long lmpc_lq_stamps[LQ_STAMP_QPS][LQ_STAMP_N];
 #define LQ_STAMP_DECL unsigned long long _lq_acc[LQ_STAMP_N] = {}; unsigned long long _lq_t0 = __builtin_readcyclecounter();
 #define LQ_STAMP(i) do { const unsigned long long _t = __builtin_readcyclecounter(); _lq_acc[i] += _t - _lq_t0; _lq_t0 = _t; } while (0)
 #define LQ_STAMP_FLUSH(qp) do { if (threadIdx.x == 0 && (qp) < LQ_STAMP_QPS) for (int _i = 0; _i < LQ_STAMP_N; ++_i) lmpc_lq_stamps[qp][_i] = _lq_acc[_i]; } while (0)
+#define LQ_MARK(v) const unsigned long long v = __builtin_readcyclecounter()
+#define LQ_ADD_SINCE(i, v) do { _lq_acc[i] += __builtin_readcyclecounter() - (v); } while (0)
 #else
+#define LQ_MARK(v) do {} while (0)
+#define LQ_ADD_SINCE(i, v) do {} while (0)
 #define LQ_STAMP_DECL
 #define LQ_STAMP(i) do {} while (0)
 #define LQ_STAMP_FLUSH(qp) do {} while (0)
@@ -223,6 +227,14 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     // the serial sweeps load a stage's operands one stage ahead in the lone-wave instance (its latency is
     // nobody else's to hide); at two waves per SIMD the second set of registers would spill instead
     constexpr bool LQ_PF = WPE == 1;
+    // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: they pay where stages have three or
+    // four stance legs (stand / walk, H = 10); at two leg-steps per lane (trot horizons 20-30) the extra leg-step work
+    // is not repaid
+#ifdef LMPC_LQ_RP
+    constexpr bool LQ_RP = LS == 1;
+#else
+    constexpr bool LQ_RP = false;
+#endif
     LQ_STAMP_DECL
 
     // ---- prologue: record, terrain frames, I_w^-1, G0, yaw cos / sin ----------------------------------------
@@ -397,7 +409,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 double qxl[NTQ];
     #pragma unroll
                 for (int i = 0; i < NTQ; ++i) qxl[i] = xr[min(lq_lane<WPE>(lane) + 64 * i, 12 * H - 1)];
-                double du[LS][6];
+                double du[LS][6], gq[LS][6];
                 bool cpl[LS];
     #pragma unroll
                 for (int t = 0; t < LS; ++t) {
@@ -477,10 +489,12 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     #pragma unroll
                         for (int a = 0; a < 3; ++a) sl[LQ_X + 3 * j + a] = rr[t][a];
                     }
-                    if (md != POLISH) {
-                        // the interior point's Newton systems in reduced inputs (RED6 of tools/lq_proto.py): with
-                        // Rr = L L' (lane-local), Y = G0_j L^-T: the leg's W_j = Y Y' and g_j = Y L^-1 rr (-du, summed
-                        // over the stage's legs below); swing legs add nothing
+                    if (md != POLISH || LQ_RP) {
+                        // the Newton systems in reduced inputs (RED6 of tools/lq_proto.py): with Rr = L L' (lane-local),
+                        // Y = Bt_j L^-T (Bt_j = G0_j T: G0_j on a stance leg in the interior point): the leg's W_j = Y Y'
+                        // and g_j = Y L^-1 rr, summed over the stage's legs below; swing legs add nothing.  The interior
+                        // point always solves in reduced inputs (W_k -> the Z field, dv - g -> dv); the polish where W_k is
+                        // well conditioned (W_k -> the K field, g_k -> the rho field; the U pre-pass decides per stage)
                         const double i00 = rsq_nr(Rr[t][0]);
                         const double l10 = Rr[t][1] * i00, l20 = Rr[t][2] * i00;
                         const double i11 = rsq_nr(fma(-l10, l10, Rr[t][3]));
@@ -494,13 +508,25 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     #pragma unroll
                         for (int m = 0; m < 6; ++m) {
                             const double g0 = G0s[m * 12 + 3 * j + 0], g1 = G0s[m * 12 + 3 * j + 1], g2 = G0s[m * 12 + 3 * j + 2];
-                            Y[m][0] = st[t] ? g0 * i00 : 0.0;
-                            Y[m][1] = st[t] ? fma(g0, m10, g1 * i11) : 0.0;
-                            Y[m][2] = st[t] ? fma(g0, m20, fma(g1, m21, g2 * i22)) : 0.0;
-                            du[t][m] = -fma(Y[m][0], c0, fma(Y[m][1], c1, Y[m][2] * c2));
+                            double b0, b1, b2;
+                            if (md == POLISH) {
+                                b0 = g0 * T[0] + g1 * T[3] + g2 * T[6];
+                                b1 = g0 * T[1] + g1 * T[4] + g2 * T[7];
+                                b2 = g0 * T[2] + g1 * T[5] + g2 * T[8];
+                            } else {
+                                b0 = st[t] ? g0 : 0.0;
+                                b1 = st[t] ? g1 : 0.0;
+                                b2 = st[t] ? g2 : 0.0;
+                            }
+                            Y[m][0] = b0 * i00;
+                            Y[m][1] = fma(b0, m10, b1 * i11);
+                            Y[m][2] = fma(b0, m20, fma(b1, m21, b2 * i22));
+                            const double gm = fma(Y[m][0], c0, fma(Y[m][1], c1, Y[m][2] * c2));
+                            if (md == POLISH) gq[t][m] = gm;
+                            else du[t][m] = -gm;
                         }
-                        if (md == PRED) {  // W_k = sum over the quad, entry by entry, to the Z field (U's place)
-                            ldouble* wz = slots + lsk[t] * LQ_SLOT + LQ_Z;
+                        if (md != CORR) {  // W_k = sum over the quad, entry by entry (U's place)
+                            ldouble* wz = slots + lsk[t] * LQ_SLOT + (md == POLISH ? LQ_K : LQ_Z);
                             const bool lead = valid[t] && j == 0;
     #pragma unroll
                             for (int m = 0; m < 6; ++m)
@@ -518,8 +544,16 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 for (int t = 0; t < LS; ++t) {
     #pragma unroll
                     for (int m = 0; m < 6; ++m) du[t][m] = quad_sum(du[t][m]);
+                    if (md == POLISH && LQ_RP) {
+    #pragma unroll
+                        for (int m = 0; m < 6; ++m) gq[t][m] = quad_sum(gq[t][m]);
+                    }
                     if (valid[t] && lsj[t] == 0) {
                         ldouble* sl = slots + lsk[t] * LQ_SLOT;
+                        if (md == POLISH && LQ_RP) {
+    #pragma unroll
+                            for (int m = 0; m < 6; ++m) sl[LQ_RHO + m] = gq[t][m];
+                        }
                         if (md == CORR) {
     #pragma unroll
                             for (int m = 0; m < 6; ++m) sl[LQ_RHO + m] = -du[t][m] + sl[LQ_DV + m] + (m == 5 ? prm.grav * dt : 0.0);
@@ -689,11 +723,16 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // interior point: reduced inputs -- B^ rows 6-11 = [U | 0 | dv'], unit input Hessian, X = L^-1 [0 | U' | 0],
                 // two 3x3 pivot blocks whatever the stage's leg count; polish: Bt, Rr_j, rr as staged by the legs
                 const bool red = mode != POLISH;
-                if (red) {
-                    // U_k = chol(W_k) for every stage at once (lane k), in place of W in the Z field; pivots at rounding
-                    // level (W is rank-deficient with fewer than two stance legs) leave a zero column
+                LQ_MARK(_lq_fact0);
+                if (red || LQ_RP) {
+                    // U_k = chol(W_k) for every stage at once (lane k), in place of W (Z field; polish: K field); pivots
+                    // at rounding level (W is rank-deficient with fewer than two stance legs) leave a zero column.  The
+                    // polish solves a stage in reduced inputs only where W_k is well conditioned (every other pivot
+                    // above 1e-6 of its diagonal: a polish answer must be exact); the flag goes to the exchange buffer
                     for (int k = lq_lane<WPE>(lane); k < H; k += 64) {
-                        ldouble* wz = slots + k * LQ_SLOT + LQ_Z;
+                        ldouble* wz = slots + k * LQ_SLOT + (red ? LQ_Z : LQ_K);
+                        const double floor_ = red ? 1e-10 : 1e-12;
+                        bool wellc = true;
                         double w[21];
 #pragma unroll
                         for (int e = 0; e < 21; ++e) w[e] = wz[e];
@@ -703,7 +742,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                             double d = wd;
 #pragma unroll
                             for (int b = 0; b < c; ++b) d = fma(-w[pk6(c, b)], w[pk6(c, b)], d);
-                            const bool ok = d > 1e-10 * wd && wd > 0.0;
+                            const bool ok = d > floor_ * wd && wd > 0.0;
+                            wellc = wellc && (!ok || d > 1e-6 * wd);
                             const double inv = ok ? rsq_nr(d) : 0.0;
                             w[pk6(c, c)] = ok ? d * inv : 0.0;
 #pragma unroll
@@ -716,6 +756,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         }
 #pragma unroll
                         for (int e = 0; e < 21; ++e) wz[e] = w[e];
+                        if (!red) ex[k] = wellc ? 1.0 : 0.0;
                     }
                     LMPC_SYNC();
                 }
@@ -735,28 +776,40 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // the stage sweep, specialised for the interior point (reduced inputs) and for the polish
                 auto sweep = [&](auto red_tag) {
                     constexpr bool red = decltype(red_tag)::value;
+                    constexpr int UF = red ? LQ_Z : LQ_K;  // where U_k is (the polish stages Bt in the Z field)
                     double bg[2], xg[3], qn[3], ckn, skn;
+                    bool sfn;
                     auto fetch = [&](int k) {
                         const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                         const ldouble* sl = slots + k * LQ_SLOT;
                         ckn = cs[2 * k];
                         skn = cs[2 * k + 1];
+                        // stage k in reduced inputs? (always in the interior point; the polish's per-stage flag)
+                        const bool srf = red || (LQ_RP && __builtin_amdgcn_readfirstlane(ex[k] != 0.0 ? 1 : 0) != 0);
+                        sfn = srf;
     #pragma unroll
                         for (int kk = 0; kk < 2; ++kk) {
                             const int r = 4 * (kk + 1) + lr;
                             const int a = r - 6;
-                            // reduced: U[a][lc] (lower: lc <= a); polish: Bt[a][lc]; column 12: dv
-                            const bool in = r >= 6 && r < 12 && (lc == 12 || (red ? lc <= a : lc < 12));
-                            const int off = lc == 12 ? LQ_DV + a : (red ? LQ_Z + pk6(a, lc) : LQ_Z + a * 12 + lc);
-                            bg[kk] = (in ? sl : zero)[in ? off : 0];
+                            // reduced: U[a][lc] (lower: lc <= a); full: Bt[a][lc]; column 12: dv (a reduced polish stage:
+                            // dv - g, g in the rho field)
+                            const bool in = r >= 6 && r < 12 && (lc == 12 || (srf ? lc <= a : lc < 12));
+                            const int off = lc == 12 ? LQ_DV + a : (srf ? UF + pk6(a, lc) : LQ_Z + a * 12 + lc);
+                            double v = (in ? sl : zero)[in ? off : 0];
+                            if (!red) {
+                                const int ac = r >= 6 && r < 12 ? a : 0;
+                                const double gv = sl[LQ_RHO + ac];
+                                v -= (srf && in && lc == 12) ? gv : 0.0;
+                            }
+                            bg[kk] = v;
                         }
     #pragma unroll
                         for (int i = 0; i < 3; ++i) {
                             const int r = lr + 4 * i;
                             const int a = lc - 6;
-                            // X columns 6-11: reduced U[a][r] (r <= a), polish Bt[a][r]; column 12: rr (polish only)
-                            const bool in = lc >= 6 && (red ? (lc < 12 && r <= a) : lc <= 12);
-                            const int off = lc == 12 ? LQ_X + r : (red ? LQ_Z + pk6(a, r) : LQ_Z + a * 12 + r);
+                            // X columns 6-11: full stages Bt[a][r], column 12: rr (reduced stages: the lane-local 6x6)
+                            const bool in = !srf && lc >= 6 && lc <= 12;
+                            const int off = lc == 12 ? LQ_X + r : LQ_Z + a * 12 + r;
                             xg[i] = (in ? sl : zero)[in ? off : 0];
                         }
                         const int km = k > 0 ? k - 1 : 0;
@@ -771,6 +824,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                         ldouble* sl = slots + k * LQ_SLOT;
                         const double ck = ckn, sk = skn;
+                        const bool sr = red || sfn;
                         double bh[2], xb[3], qc[3];
     #pragma unroll
                         for (int kk = 0; kk < 2; ++kk) bh[kk] = bg[kk];
@@ -799,13 +853,13 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         __builtin_amdgcn_sched_barrier(0);
                         // reduced inputs: this lane's U row (c = lc - 6, for its X columns), read before Z_k overwrites U_k
                         double ur[6];
-                        if (red) {
+                        if (sr) {
                             const bool xc = lc >= 6 && lc < 12;
                             const int ac = xc ? lc - 6 : 0;
     #pragma unroll
                             for (int b = 0; b < 6; ++b) {
                                 const bool in = xc && b <= ac;
-                                ur[b] = (in ? sl : zero)[in ? LQ_Z + pk6(ac, b) : 0];
+                                ur[b] = (in ? sl : zero)[in ? UF + pk6(ac, b) : 0];
                             }
                         }
                         // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
@@ -825,7 +879,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         d4 X;
                         const int ls0 = 4 * k;
                         const int lmask = (int)(((LS == 1 || ls0 < 64 ? cmask[0] : cmask[LS - 1]) >> (ls0 & 63)) & 15ull);  // static indices: a dynamically indexed array lives in scratch
-                        if (red) {
+                        if (sr) {
                             // ---- reduced inputs: Guu' = I + U'P22 U (6 x 6) through LDS once, factored by every lane
                             // (Guu' >= I: no pivot can fail), X = L^-1 U' (rows 0-5, columns 6-11): each lane solves L y = its U
                             // row and keeps its own rows of y; a stage without stance legs has U = 0 and X = 0 ----
@@ -957,7 +1011,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         for (int i = 1; i < 3; ++i) {
                             const int r = lr + 4 * i;
                             const bool zr = r >= 6 && r < 12;
-                            const bool ko = zr && ((lc >= 6 && lc < 12 && lc <= r) || lc == 12);
+                            // (a reduced polish stage keeps g in the rho field: its rho is 0, and dv - g is its d)
+                            const bool ko = zr && ((lc >= 6 && lc < 12 && lc <= r) || (lc == 12 && (red || !sr)));
                             const int off = lc == 12 ? LQ_RHO + (r - 6) : LQ_K + pk6(r - 6, lc - 6);
                             (ko ? sl : sink)[ko ? off : lane] = KH[i];
                         }
@@ -978,7 +1033,9 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                                     const int r = lr + 4 * i;
                                     const bool zr = r >= 6 && r < 12 && lc <= 12;
                                     ldouble* dst = lc == 12 ? sl + LQ_RHO + (r - 6) : kzr + k * 72 + (r - 6) * 12 + lc;
-                                    (zr ? dst : sink + lane)[0] = KZ[i];
+                                    // t = K za + rho; a reduced polish stage: K za + g (g in the rho field)
+                                    const double gadd = (!red && sr && lc == 12) ? sl[LQ_RHO + (zr && lc == 12 ? r - 6 : 0)] : 0.0;
+                                    (zr ? dst : sink + lane)[0] = KZ[i] + gadd;
                                 }
                             }
                         }
@@ -1004,6 +1061,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 if (mode != POLISH) sweep(std::true_type{});
                 else sweep(std::false_type{});
                 LMPC_SYNC();
+                if (!red) LQ_ADD_SINCE(15, _lq_fact0);  // the polish's factorisations (also counted in 11-14, 3)
                 LQ_STAMP(3);  // factorisation
             }
 

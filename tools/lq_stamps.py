@@ -25,10 +25,10 @@ buf = buf.astype(float)
 ipm = (it[:n] & 0xffff).astype(float)
 rnd = (it[:n] >> 16).astype(float)
 calls = {0: np.ones(n), 1: 2 * ipm + rnd, 2: ipm, 3: ipm + rnd, 4: 2 * ipm + rnd, 5: 2 * ipm + rnd, 6: ipm, 7: ipm,
-         8: rnd, 9: rnd, 10: np.ones(n), 11: ipm + rnd, 12: ipm + rnd, 13: ipm + rnd, 14: ipm + rnd, 15: ipm + rnd}
+         8: rnd, 9: rnd, 10: np.ones(n), 11: ipm + rnd, 12: ipm + rnd, 13: ipm + rnd, 14: ipm + rnd, 15: rnd}
 names = ["prologue", "leg-step work", "corr backward", "factorisation", "forward sweep", "inputs", "pred step",
-         "corr step", "adjoint", "polish check", "epilogue", " f:C,PA,G", " f:leg blocks", " f:KH", " f:KZ,P", " f:S"]
-tot = buf[:, :16].sum(1)
+         "corr step", "adjoint", "polish check", "epilogue", " f:C,PA,G", " f:leg blocks", " f:KH", " f:KZ,P", " f:polish (incl.)"]
+tot = buf[:, :15].sum(1)
 print(f"LDS kernel: config {cid} H={H} B={count}: mean cycles/QP {tot.mean():.0f} max {tot.max():.0f}  "
       f"ipm {ipm.mean():.2f} rounds {rnd.mean():.2f}")
 for i, nm in enumerate(names):
