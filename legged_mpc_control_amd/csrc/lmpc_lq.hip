@@ -227,14 +227,10 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     // the serial sweeps load a stage's operands one stage ahead in the lone-wave instance (its latency is
     // nobody else's to hide); at two waves per SIMD the second set of registers would spill instead
     constexpr bool LQ_PF = WPE == 1;
-    // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: they pay where stages have three or
-    // four stance legs (stand / walk, H = 10); at two leg-steps per lane (trot horizons 20-30) the extra leg-step work
-    // is not repaid
-#ifdef LMPC_LQ_RP
-    constexpr bool LQ_RP = LS == 1;
-#else
-    constexpr bool LQ_RP = false;
-#endif
+    // reduced-input polish stages (well-conditioned W_k) in the two-wave instance: measured -1.2 % on config 4 (stages
+    // with three or four stance legs); in the lone-wave instance (+2.5 % on config 2 with the dense path off: a trot's
+    // full polish stage has only two pivot blocks) and at two leg-steps per lane they are not repaid
+    constexpr bool LQ_RP = LS == 1 && WPE == 2;
     LQ_STAMP_DECL
 
     // ---- prologue: record, terrain frames, I_w^-1, G0, yaw cos / sin ----------------------------------------
