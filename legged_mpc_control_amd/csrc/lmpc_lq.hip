@@ -219,7 +219,9 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     ldouble* const cs = sm + LQF_CS;
     ldouble* const slots = sm + LQF_FIXED + 2 * H;
     ldouble* const kzr = slots + LQ_SLOT * H;  // closed-loop rows (kzs only)
-    const bool kzs = LS == 1 && WPE == 2 && lq_kzs(H);  // measured: a gain at two waves per SIMD only
+    // (both instances, although it pays only at two waves per SIMD: the instance a QP runs on depends on the batch,
+    // and a QP's answer must not -- test_full_size_properties checks the bits)
+    const bool kzs = LS == 1 && lq_kzs(H);
     const int RL = 33 + 12 * H;
     const double* rin = rec + (size_t)qp * RL;
     const double* xr = rin + 33;  // x_ref (global, L2-resident after its first use)
@@ -227,10 +229,10 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     // the serial sweeps load a stage's operands one stage ahead in the lone-wave instance (its latency is
     // nobody else's to hide); at two waves per SIMD the second set of registers would spill instead
     constexpr bool LQ_PF = WPE == 1;
-    // reduced-input polish stages (well-conditioned W_k) in the two-wave instance: measured -1.2 % on config 4 (stages
-    // with three or four stance legs); in the lone-wave instance (+2.5 % on config 2 with the dense path off: a trot's
-    // full polish stage has only two pivot blocks) and at two leg-steps per lane they are not repaid
-    constexpr bool LQ_RP = LS == 1 && WPE == 2;
+    // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: measured -1.2 % on config 4 (stages
+    // with three or four stance legs), +2.5 % on config 2 with the dense path off (a trot's full polish stage has only
+    // two pivot blocks); both instances alike, as kzs above; at two leg-steps per lane the leg-step work is not repaid
+    constexpr bool LQ_RP = LS == 1;
     LQ_STAMP_DECL
 
     // ---- prologue: record, terrain frames, I_w^-1, G0, yaw cos / sin ----------------------------------------
