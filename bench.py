@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the second timed pass that also gathers all GRFs to rank 0")
     ap.add_argument("--dense", choices=["ipm", "gi", "off"], default=None,
-                    help="dense-path kernel (lmpc_set_dense_path); default ipm")
+                    help="dense-path kernel (lmpc_set_dense_path); default ipm, config 4: off")
     ap.add_argument("--riccati", choices=["lds", "scratch"], default="lds",
                     help="Riccati kernel of the QPs no dense kernel takes (lmpc_set_riccati_path); default lds")
     ap.add_argument("--index-offset", type=int, default=0,
@@ -126,10 +126,13 @@ def main():
     # Inputs are generated ON THE DEVICE from (seed, global index): every rank builds its own shard in
     # HBM, no input bytes cross PCIe or xGMI.  Commands -> records + contact schedules
     # by the expansion kernel (8f-1); the timed step below is the QP solve over those records.
-    # Dense-path kernel: the interior point for every workload since the round-3 hand-over rework (DESIGN.md 2.4;
-    # config 4 13.8 ms against 15.1 ms on the dual active set, profiles/r03/handover/ab_c4_dense.log).  Fixed per
-    # context, so no answer depends on it; --dense overrides it.
-    dense = args.dense or "ipm"
+    # Dense-path kernel: the interior point where the batch is small enough that the Riccati kernel
+    # runs one wave per SIMD (config 2: 0.18 ms against 0.31 ms on the Riccati kernel alone); config 4's 65536 QPs
+    # go to the Riccati kernel alone, whose two-wave instance solves its trot QPs faster than the dense kernel's
+    # one wave per SIMD does (round 4, DESIGN.md 4d: 9.8 ms against 10.5 ms split).  Fixed per context, so no
+    # answer depends on the batch or the shard; --dense overrides it.
+    default_dense = "off" if args.config == 4 else "ipm"
+    dense = args.dense or default_dense
     solver = BatchedConvexQPSolver(p, H, max_batch=0, device=local_rank, dense_path=dense, riccati_path=args.riccati)
     opts = {}
     for kv in args.opt:
@@ -295,7 +298,7 @@ def main():
     executed = None
     # the committed PMC figures are keyed by workload, plus "/<mode>" when --dense overrides the config's own path
     # (configs 3 and 5 run the Riccati kernel by default: H > 16 has no dense path)
-    overridden = args.dense is not None and args.dense != "ipm"
+    overridden = args.dense is not None and args.dense != default_dense
     wl = (f"{wl_name}/{mode}" if overridden else wl_name) if args.batch is None else None
     if wl is not None and args.riccati != "lds":
         wl += "/scratch"

@@ -130,6 +130,21 @@ __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, doub
     return x[r];
 }
 
+// The factorisation sweep reads the lane index once per sweep (bit 0: for the stage body, bit 1: for the operand
+// fetch), so its lane-static offsets and masks are computed once per sweep instead of once per stage (478 -> 187
+// instructions per stage).  That fits 256 registers at two waves per SIMD only because every other pass takes its
+// own opaque copy of the lane index (no lane address lives across the sweep) and the reduced stage reads its U row
+// late (LMPC_LQ_LATE); config 4 10.8 -> 9.9 ms.  0 restores the per-stage maps (diagnostic).
+#ifndef LMPC_LQ_HOIST
+#define LMPC_LQ_HOIST 3
+#endif
+// The reduced stage reads its U row after the pivot staging and stores Z_k after the solve (shorter live ranges
+// across the 6 x 6 factor); 0 = read U before the Z_k stores (diagnostic)
+#ifndef LMPC_LQ_LATE
+#define LMPC_LQ_LATE 1
+#endif
+constexpr bool LQ_LATE = LMPC_LQ_LATE != 0;
+
 __device__ __forceinline__ int lq_opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
@@ -631,8 +646,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         if (e < 12 * (H - 1)) slots[(k - 1) * LQ_SLOT + LQ_X + r] = v;
                     }
                     LMPC_SYNC();
-                    const int r = lane < 12 ? lane : 0;
-                    double p = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
+                    const int lnb = lq_lane<WPE>(lane), r = lnb < 12 ? lnb : 0;  // per pass: no lane address outlives it
+                    double p = lnb < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
                     for (int k = H - 1; k >= 0; --k) {
                         const ldouble* sl = slots + k * LQ_SLOT;
                         const double y = p + sl[LQ_V + r];
@@ -641,8 +656,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
 #pragma unroll
                         for (int a = 0; a < 6; ++a) kz[a] = kzr[k * 72 + a * 12 + r];
                         const double q = slots[kp * LQ_SLOT + LQ_X + r], ck = cs[2 * k], sk = cs[2 * k + 1];
-                        if (lane < 12) ex[r] = y;
-                        if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
+                        if (lnb < 12) ex[r] = y;
+                        if (lnb >= 6 && lnb < 12) slots[k * LQ_SLOT + LQ_Z + (lnb - 6) * 13 + 12] = y;
                         LMPC_SYNC();
                         if (k == 0) break;
                         double pn = q + lq_row_apply(ex, r, lq_atw_row(r, ck, sk), dt);
@@ -668,8 +683,8 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 // backward: y = p_{k+1} + v_k, za = y[6:12] -> Z column 12, t = K za + rho, p_k = q_k + A'y - Z't.
                 // Lanes 0-11 hold p (lane r <-> p[r]); y goes through the exchange buffer, t by readlane.
                 {
-                    const int r = lane < 12 ? lane : 0;
-                    const int m = lane < 6 ? lane : 0;
+                    const int lnb = lq_lane<WPE>(lane), r = lnb < 12 ? lnb : 0;
+                    const int m = lnb < 6 ? lnb : 0;
                     // a stage's operands are loaded while the stage before it runs: an LDS load cannot move above
                     // the fence that orders the exchange buffer, so loaded in the stage itself they would wait a
                     // round trip on the serial path
@@ -690,12 +705,12 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                     };
                     BwOps cur, nxt;
                     load(H - 1, cur);
-                    double p = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
+                    double p = lnb < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
                     for (int k = H - 1; k >= 0; --k) {
                         if (!LQ_PF && k < H - 1) load(k, cur);
                         const double y = p + cur.v;
-                        if (lane < 12) ex[r] = y;
-                        if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_Z + (lane - 6) * 13 + 12] = y;
+                        if (lnb < 12) ex[r] = y;
+                        if (lnb >= 6 && lnb < 12) slots[k * LQ_SLOT + LQ_Z + (lnb - 6) * 13 + 12] = y;
                         if (LQ_PF && k > 0) load(k - 1, nxt);
                         LMPC_SYNC();
                         if (k == 0) break;
@@ -775,10 +790,11 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 auto sweep = [&](auto red_tag) {
                     constexpr bool red = decltype(red_tag)::value;
                     constexpr int UF = red ? LQ_Z : LQ_K;  // where U_k is (the polish stages Bt in the Z field)
+                    const int sfl = lq_lane<WPE>(lane);  // one lane read for the whole sweep (its offsets stay in registers)
                     double bg[2], xg[3], qn[3], ckn, skn;
                     bool sfn;
                     auto fetch = [&](int k) {
-                        const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
+                        const int fl = (LMPC_LQ_HOIST & 2) ? sfl : lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                         const ldouble* sl = slots + k * LQ_SLOT;
                         ckn = cs[2 * k];
                         skn = cs[2 * k + 1];
@@ -819,7 +835,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                     };
                     fetch(H - 1);
                     for (int k = H - 1; k >= 0; --k) {
-                        const int fl = lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
+                        const int fl = (LMPC_LQ_HOIST & 1) ? sfl : lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                         ldouble* sl = slots + k * LQ_SLOT;
                         const double ck = ckn, sk = skn;
                         const bool sr = red || sfn;
@@ -851,7 +867,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         __builtin_amdgcn_sched_barrier(0);
                         // reduced inputs: this lane's U row (c = lc - 6, for its X columns), read before Z_k overwrites U_k
                         double ur[6];
-                        if (sr) {
+                        auto read_ur = [&]() {
                             const bool xc = lc >= 6 && lc < 12;
                             const int ac = xc ? lc - 6 : 0;
     #pragma unroll
@@ -859,20 +875,24 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                                 const bool in = xc && b <= ac;
                                 ur[b] = (in ? sl : zero)[in ? UF + pk6(ac, b) : 0];
                             }
-                        }
+                        };
+                        if (!LQ_LATE && sr) read_ur();
                         // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
                         if (lc == 12) {
     #pragma unroll
                             for (int i = 0; i < 3; ++i) PA[i] += C[i];
                         }
     #pragma unroll
-                        for (int i = 0; i < 3; ++i) (lc == 12 ? sl : sink)[lc == 12 ? LQ_V + lr + 4 * i : lane] = C[i];
+                        for (int i = 0; i < 3; ++i) (lc == 12 ? sl : sink)[lc == 12 ? LQ_V + lr + 4 * i : fl] = C[i];
+                        auto store_z = [&]() {
     #pragma unroll
-                        for (int i = 1; i < 3; ++i) {
-                            const int r = lr + 4 * i;
-                            const bool o = r >= 6 && r < 12 && lc <= 12;
-                            (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : lane] = PA[i];
-                        }
+                            for (int i = 1; i < 3; ++i) {
+                                const int r = lr + 4 * i;
+                                const bool o = r >= 6 && r < 12 && lc <= 12;
+                                (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : fl] = PA[i];
+                            }
+                        };
+                        if (!LQ_LATE) store_z();
                         LQ_STAMP(11);  // factorisation: C, PA, G, Z / v stores
                         d4 X;
                         const int ls0 = 4 * k;
@@ -888,6 +908,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                                 if (lc < 6 && r < 6) pv[r * 6 + lc] = G[i];
                             }
                             LMPC_SYNC();
+                            if (LQ_LATE) read_ur();  // U_k is still in place: Z_k is stored after the solve below
                             double gl[21];
     #pragma unroll
                             for (int r = 0; r < 6; ++r)
@@ -948,22 +969,22 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                             // previous block's reads of the staging rows before these writes)
                             LMPC_SYNC();
                             {
-                                ldouble* dt0 = ina ? pv + 16 * ra + lc : sink + lane;
+                                ldouble* dt0 = ina ? pv + 16 * ra + lc : sink + fl;
                                 dt0[0] = Tg[i0];
                                 if (i1 != i0) {
-                                    ldouble* dt1 = inb ? pv + 16 * rb + lc : sink + lane;
+                                    ldouble* dt1 = inb ? pv + 16 * rb + lc : sink + fl;
                                     dt1[0] = Tg[i1];
                                 }
-                                ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + lane;
+                                ldouble* da = ina ? pv + 48 + 16 * ra + lc : sink + fl;
                                 da[0] = Li[i0];
-                                ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + lane;
+                                ldouble* dx = ina ? pv + 96 + 16 * ra + lc : sink + fl;
                                 dx[0] = X[i0];
                                 Li[i0] = ina ? 0.0 : Li[i0];
                                 X[i0] = ina ? 0.0 : X[i0];
                                 if (i1 != i0) {
-                                    ldouble* db = inb ? pv + 48 + 16 * rb + lc : sink + lane;
+                                    ldouble* db = inb ? pv + 48 + 16 * rb + lc : sink + fl;
                                     db[0] = Li[i1];
-                                    ldouble* dy = inb ? pv + 96 + 16 * rb + lc : sink + lane;
+                                    ldouble* dy = inb ? pv + 96 + 16 * rb + lc : sink + fl;
                                     dy[0] = X[i1];
                                     Li[i1] = inb ? 0.0 : Li[i1];
                                     X[i1] = inb ? 0.0 : X[i1];
@@ -1000,11 +1021,16 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                             X = MFMA64(aw, bx, X);
                         }
                         }
+                        if (LQ_LATE) {
+                            LMPC_SYNC();  // every lane's U_k reads ahead of the Z_k stores over them
+                            store_z();
+                        }
                         LQ_STAMP(12);  // factorisation: leg blocks
                         // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
                         d4 KH = {0.0, 0.0, 0.0, 0.0};
     #pragma unroll
-                        for (int kk = 0; kk < 3; ++kk) KH = MFMA64(X[kk], X[kk], KH);
+                        for (int kk = 0; kk < 2; ++kk) KH = MFMA64(X[kk], X[kk], KH);
+                        if (!sr) KH = MFMA64(X[2], X[2], KH);  // reduced inputs: X has rows 0-5 only
     #pragma unroll
                         for (int i = 1; i < 3; ++i) {
                             const int r = lr + 4 * i;
@@ -1012,7 +1038,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                             // (a reduced polish stage keeps g in the rho field: its rho is 0, and dv - g is its d)
                             const bool ko = zr && ((lc >= 6 && lc < 12 && lc <= r) || (lc == 12 && (red || !sr)));
                             const int off = lc == 12 ? LQ_RHO + (r - 6) : LQ_K + pk6(r - 6, lc - 6);
-                            (ko ? sl : sink)[ko ? off : lane] = KH[i];
+                            (ko ? sl : sink)[ko ? off : fl] = KH[i];
                         }
                         LQ_STAMP(13);  // factorisation: KH, K / rho stores
                         d4 KZ = {0.0, 0.0, 0.0, 0.0};
@@ -1033,7 +1059,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                                     ldouble* dst = lc == 12 ? sl + LQ_RHO + (r - 6) : kzr + k * 72 + (r - 6) * 12 + lc;
                                     // t = K za + rho; a reduced polish stage: K za + g (g in the rho field)
                                     const double gadd = (!red && sr && lc == 12) ? sl[LQ_RHO + (zr && lc == 12 ? r - 6 : 0)] : 0.0;
-                                    (zr ? dst : sink + lane)[0] = KZ[i] + gadd;
+                                    (zr ? dst : sink + fl)[0] = KZ[i] + gadd;
                                 }
                             }
                         }
@@ -1172,7 +1198,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         const double xn = xa + (r >= 6 ? k0 + k1 : 0.0);
                         if (LQ_PF) cur = nxt;
                         LMPC_SYNC();
-                        if (lane < 12) {
+                        if (ln < 12) {
                             ex[16 + r] = xn;
                             slots[k * LQ_SLOT + LQ_X + r] = xn;
                         }
@@ -1331,7 +1357,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 {
                     // tracking terms q (x_k - x_ref,k-1) of every stage at once -> x slot (dead after this), then the
                     // serial sweep lambda_k = q_k-term + A_k' lambda_{k+1}, lambda_{k+1}[6:12] -> rho slot k
-                    const int r = lane < 12 ? lane : 0;
+                    const int lnv = lq_lane<WPE>(lane), r = lnv < 12 ? lnv : 0;
                     {
                         constexpr int NTQ = LS == 1 ? 3 : 6;
                         double xl[NTQ];
@@ -1347,10 +1373,10 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         }
                         LMPC_SYNC();
                     }
-                    double lam = lane < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
+                    double lam = lnv < 12 ? slots[(H - 1) * LQ_SLOT + LQ_X + r] : 0.0;
                     for (int k = H - 1; k >= 0; --k) {
-                        if (lane < 12) ex[r] = lam;
-                        if (lane >= 6 && lane < 12) slots[k * LQ_SLOT + LQ_RHO + (lane - 6)] = lam;
+                        if (lnv < 12) ex[r] = lam;
+                        if (lnv >= 6 && lnv < 12) slots[k * LQ_SLOT + LQ_RHO + (lnv - 6)] = lam;
                         // the stage's own operands ahead of the fence (they do not depend on the exchange)
                         const int kp = k > 0 ? k - 1 : 0;
                         const double q = slots[kp * LQ_SLOT + LQ_X + r], ck = cs[2 * k], sk = cs[2 * k + 1];

@@ -328,6 +328,44 @@ def test_failure_statuses_stay_per_chain(hq):
     assert np.all(st == 0) and np.array_equal(x, x0)
 
 
+@pytest.mark.parametrize("tol_mu", [1e-4, 1e-6])
+def test_failed_crossover_below_an_exact_level_meets_the_true_bounds(hq, tol_mu):
+    """A level whose crossover does not verify keeps its interior-point iterate; if a level above took its
+    crossover answer, this level's interior point ran against frozen bounds raised by the tight-row margin
+    (lmpc_hoqp.hip, hb_true).  Its status must then be judged against the TRUE bounds: a level reported converged
+    meets every higher-priority inequality d_j x <= f_j + w_j within tol_res of the scale, else it reports
+    LMPC_QP_MAX_ITER.  A loose tol_mu (single pass: above the two-pass hand-over) makes the crossover miss on some
+    levels of the golden groups, which is the path under test."""
+    hit = 0
+    for group in ("wbc", "rand3", "n20", "n64", "exhaust"):
+        g = load(group)
+        dims = dims_from(g["dims"])
+        B = g["rec"].shape[0]
+        solver = hq.HoqpBatch(dims, B)
+        solver.set_options(tol_mu=tol_mu)
+        x, w, st, it = solver.solve(g["rec"])
+        xo = it >> 16
+        assert np.all(st <= 1) and np.all(np.isfinite(x)) and np.all(w >= 0.0)
+        for b in range(B):
+            levels = unpack(g["rec"][b], dims)
+            scale = 1.0 + float(np.max(np.abs(g["rec"][b])))
+            for l in range(1, dims.num_levels):
+                if not (xo[b, l] == 1 and np.any(xo[b, :l] == 3)):
+                    continue
+                hit += 1
+                if st[b] != 0:
+                    continue
+                o = 0
+                for j in range(l):
+                    d, f = levels[j][2], levels[j][3]
+                    s = d.shape[0]
+                    if s:
+                        viol = float(np.max(d @ x[b, l] - f - w[b, o:o + s]))
+                        assert viol <= 1e-7 * scale, f"{group}[{b}] level {l}: level {j} row violated by {viol:.2e}"
+                    o += s
+    print(f"tol_mu {tol_mu:g}: {hit} levels below an exact level kept a failed crossover's iterate")
+
+
 def test_crossover_off_keeps_the_interior_point_iterate(hq):
     """lmpc_hoqp_options.crossover = 0: no level tries the crossover (bits 16-17 clear) and the WBC still meets 1e-6
     from the interior point alone; with the default every WBC level's crossover verifies and the answer is exact to
