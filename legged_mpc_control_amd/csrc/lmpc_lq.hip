@@ -138,12 +138,13 @@ __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, doub
 #ifndef LMPC_LQ_HOIST
 #define LMPC_LQ_HOIST 3
 #endif
-// The reduced stage reads its U row after the pivot staging and stores Z_k after the solve (shorter live ranges
-// across the 6 x 6 factor); 0 = read U before the Z_k stores (diagnostic)
+// At two waves per SIMD the reduced stage reads its U row after the pivot staging and stores Z_k after the solve
+// (shorter live ranges across the 6 x 6 factor; the lone-wave instances keep the early read, 2 % faster there -- the
+// same arithmetic either way, so every instance gives the same bits); 0 = the early read everywhere (diagnostic)
 #ifndef LMPC_LQ_LATE
 #define LMPC_LQ_LATE 1
 #endif
-constexpr bool LQ_LATE = LMPC_LQ_LATE != 0;
+constexpr bool LQ_LATE_ON = LMPC_LQ_LATE != 0;
 
 __device__ __forceinline__ int lq_opaque(int v) {
     asm volatile("" : "+v"(v));
@@ -244,6 +245,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     // the serial sweeps load a stage's operands one stage ahead in the lone-wave instance (its latency is
     // nobody else's to hide); at two waves per SIMD the second set of registers would spill instead
     constexpr bool LQ_PF = WPE == 1;
+    constexpr bool LQ_LATE = LQ_LATE_ON && WPE == 2;
     // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: measured -1.2 % on config 4 (stages
     // with three or four stance legs), +2.5 % on config 2 with the dense path off (a trot's full polish stage has only
     // two pivot blocks); both instances alike, as kzs above; at two leg-steps per lane the leg-step work is not repaid
@@ -876,7 +878,9 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                                 ur[b] = (in ? sl : zero)[in ? UF + pk6(ac, b) : 0];
                             }
                         };
-                        if (!LQ_LATE && sr) read_ur();
+                        if constexpr (!LQ_LATE) {
+                            if (sr) read_ur();
+                        }
                         // PA column 12 += v = P d (C column 12); out: v, Z = rows 6-11 of PA (columns 0-12)
                         if (lc == 12) {
     #pragma unroll
@@ -884,15 +888,14 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         }
     #pragma unroll
                         for (int i = 0; i < 3; ++i) (lc == 12 ? sl : sink)[lc == 12 ? LQ_V + lr + 4 * i : fl] = C[i];
-                        auto store_z = [&]() {
+                        if constexpr (!LQ_LATE) {
     #pragma unroll
                             for (int i = 1; i < 3; ++i) {
                                 const int r = lr + 4 * i;
                                 const bool o = r >= 6 && r < 12 && lc <= 12;
                                 (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : fl] = PA[i];
                             }
-                        };
-                        if (!LQ_LATE) store_z();
+                        }
                         LQ_STAMP(11);  // factorisation: C, PA, G, Z / v stores
                         d4 X;
                         const int ls0 = 4 * k;
@@ -908,7 +911,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                                 if (lc < 6 && r < 6) pv[r * 6 + lc] = G[i];
                             }
                             LMPC_SYNC();
-                            if (LQ_LATE) read_ur();  // U_k is still in place: Z_k is stored after the solve below
+                            if constexpr (LQ_LATE) read_ur();  // U_k is still in place: Z_k is stored after the solve below
                             double gl[21];
     #pragma unroll
                             for (int r = 0; r < 6; ++r)
@@ -1021,16 +1024,23 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                             X = MFMA64(aw, bx, X);
                         }
                         }
-                        if (LQ_LATE) {
+                        if constexpr (LQ_LATE) {
                             LMPC_SYNC();  // every lane's U_k reads ahead of the Z_k stores over them
-                            store_z();
+    #pragma unroll
+                            for (int i = 1; i < 3; ++i) {
+                                const int r = lr + 4 * i;
+                                const bool o = r >= 6 && r < 12 && lc <= 12;
+                                (o ? sl : sink)[o ? LQ_Z + (r - 6) * 13 + lc : fl] = PA[i];
+                            }
                         }
                         LQ_STAMP(12);  // factorisation: leg blocks
                         // ---- KH = X'X: K (rows / columns 6-11, packed), rho (column 12) ----
                         d4 KH = {0.0, 0.0, 0.0, 0.0};
     #pragma unroll
                         for (int kk = 0; kk < 2; ++kk) KH = MFMA64(X[kk], X[kk], KH);
-                        if (!sr) KH = MFMA64(X[2], X[2], KH);  // reduced inputs: X has rows 0-5 only
+                        // reduced inputs: X has rows 0-5 only (one leg-step per lane: the two-leg-step instance keeps
+                        // the third product, whose code layout measured 1 % faster there)
+                        if (LS == 2 || !sr) KH = MFMA64(X[2], X[2], KH);
     #pragma unroll
                         for (int i = 1; i < 3; ++i) {
                             const int r = lr + 4 * i;
