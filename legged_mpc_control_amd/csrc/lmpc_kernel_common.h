@@ -57,11 +57,14 @@ typedef __attribute__((address_space(3))) double ldouble;
 typedef __attribute__((address_space(1))) double gdouble;
 
 // ---- wave reductions without LDS: DPP inside 16-lane rows, readlane across the 4 rows ----
+// Every DPP move here has old = 0, so bound_ctrl (an invalid source lane reads 0) gives the same value as keeping
+// old; with it set the compiler drops the v_mov that initialises old (-300 instructions in the two-wave Riccati
+// kernel, 1-2 % on configs 2-5)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, true);
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double readlane_f64(double v, int l) {
