@@ -49,10 +49,12 @@
 extern "C" {
 #endif
 
-#define LMPC_ABI_VERSION 6 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
+#define LMPC_ABI_VERSION 7 /* 2: terrain-normal extension (_ex entry points); 3: dense-path selection;
                               4: warm start (lmpc_solve_batch_warm, lmpc_shift_active_set);
                               5: dense-path caps in lmpc_options, no environment overrides;
-                              6: Riccati-kernel selection (lmpc_set_riccati_path) */
+                              6: Riccati-kernel selection (lmpc_set_riccati_path);
+                              7: per-leg gait phases in lmpc_command (lmpc_contact_schedule_legs), the polish's
+                                 KKT certificate (lmpc_options.tol_x) */
 #define LMPC_MAX_HORIZON 32
 
 /* return codes (API level) */
@@ -63,9 +65,13 @@ extern "C" {
 #define LMPC_ERR_LAUNCH (-4)
 #define LMPC_ERR_NOT_BUILT (-5)
 
-/* per-QP status codes (status[b]) */
+/* per-QP status codes (status[b]).  LMPC_QP_CONVERGED is a KKT certificate (ABI 7): the returned forces are primal
+ * feasible (pyramid and bound rows within tol_p * f_max), the state trajectory the solver used is their dynamics
+ * (x_{k+1} = A_k x_k + B u_k - g dt e11 within tol_x of the state scale), and along it the gradient has no component
+ * on any stance leg-step's free directions (within tol_d of the gradient scale) and non-negative multipliers on its
+ * active faces -- i.e. the exact optimum of the reference's QP to those tolerances. */
 #define LMPC_QP_CONVERGED 0
-#define LMPC_QP_MAX_ITER 1 /* best iterate returned */
+#define LMPC_QP_MAX_ITER 1 /* no certified optimum: the best (feasible) interior-point iterate returned */
 #define LMPC_QP_NAN 2      /* zeros returned, as the reference does (ConvexQPSolver.cpp:321-326) */
 
 #define LMPC_REC_X0 0
@@ -105,6 +111,10 @@ typedef struct lmpc_options {
     int dense_iter_cap;    /* condensed interior point: iterations before the hand-over (default 0 = none) */
     int dense_polish_iter; /* condensed interior point: first-attempt iterations before the polish (default 40) */
     int warm_rounds;       /* warm start: polish rounds before the cold fallback (default 12) */
+    /* ABI 7: the certificate's dynamics check -- the Riccati kernels' state trajectory against the dynamics of the
+     * forces they return, relative to max(1, max |x|) (default 1e-8; the measured rounding level is <= 2e-10,
+     * DESIGN.md 2.6) */
+    double tol_x;
 } lmpc_options;
 
 /* Robot presets: gazebo_go1_convex.yaml:39-71 (+ LeggedState.cpp:146,155-160
@@ -228,6 +238,12 @@ int lmpc_current_contact(int gait, int leg, double gait_phase);
  * contact[0][j] = plan_contacts[j]; contact[i][j] = predict(gait, j, phase, speed, i*dt). */
 int lmpc_contact_schedule(int gait, double gait_phase, double gait_speed, double dt, int horizon,
                           const uint8_t plan_contacts[4], uint8_t* contact);
+/* ABI 7: the same with one phase per leg, as the reference's four leg FSMs keep them (LeggedContactFSM.h:64; each
+ * leg advances on its own in ConvexMpc::foot_update, ConvexMpc.cpp:94-104, and an early touchdown wraps that leg's
+ * phase by -1, LeggedContactFSM.cpp:61-66,214-221): contact[i][j] = predict(gait, j, gait_phase[j], speed, i*dt)
+ * (ConvexQPSolver.cpp:341-342). */
+int lmpc_contact_schedule_legs(int gait, const double gait_phase[4], double gait_speed, double dt, int horizon,
+                               const uint8_t plan_contacts[4], uint8_t* contact);
 
 /* calc_mpc_reference input packing (ConvexQPSolver.cpp:256-276). */
 typedef struct lmpc_state_in {
@@ -251,12 +267,14 @@ int lmpc_pack_record(const lmpc_params* p, int horizon, const lmpc_state_in* st,
  * One command per instance = what calc_mpc_reference and update_bound_constraints
  * read (ConvexQPSolver.cpp:254-313,329-346) plus the contact FSM state
  * (LeggedContactFSM.cpp:280-294).  The device expands commands into records and
- * contact schedules in HBM: 384 B in per instance instead of 33+12H doubles and
+ * contact schedules in HBM: 408 B in per instance instead of 33+12H doubles and
  * 4H bytes, and no host preprocessing.  The expansion is bit-identical to
- * lmpc_pack_record + lmpc_contact_schedule on the host. */
+ * lmpc_pack_record + lmpc_contact_schedule_legs on the host. */
 typedef struct lmpc_command {
     lmpc_state_in state;
-    double gait_phase;        /* FSM phase in [0, 1) */
+    double gait_phase[4];     /* per-leg FSM phase (FL, FR, RL, RR; ABI 7), nominally in [0, 1); a leg that touched
+                                 down early carries its wrapped phase (below 0), as LeggedContactFSM::common_enter
+                                 leaves it (LeggedContactFSM.cpp:214-221) */
     double gait_speed;        /* phase per second */
     int32_t gait;             /* LMPC_GAIT_* */
     uint8_t plan_contacts[4]; /* step-0 contacts (ctrl.plan_contacts) */

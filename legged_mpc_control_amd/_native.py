@@ -35,8 +35,10 @@ EXPORTED_SYMBOLS = (
     "lmpc_leg_kin_default", "lmpc_foot_jacobian", "lmpc_grf_to_torque", "lmpc_grf_to_torque_device",
     # ABI 3: dense-path selection
     "lmpc_set_dense_path", "lmpc_get_dense_path", "lmpc_set_riccati_path", "lmpc_get_riccati_path",
+    # ABI 7: per-leg gait phases
+    "lmpc_contact_schedule_legs",
 )
-ABI_VERSION = 6
+ABI_VERSION = 7
 # include/lmpc/lmpc_hoqp.h: batched hierarchical QP (whole-body control)
 HOQP_SYMBOLS = (
     "lmpc_hoqp_dims_wbc", "lmpc_hoqp_options_default", "lmpc_hoqp_record_len", "lmpc_hoqp_slack_len",
@@ -82,6 +84,8 @@ class LmpcOptions(ctypes.Structure):
         ("dense_iter_cap", ctypes.c_int),
         ("dense_polish_iter", ctypes.c_int),
         ("warm_rounds", ctypes.c_int),
+        # ABI 7: the certificate's dynamics check (relative to the state scale)
+        ("tol_x", ctypes.c_double),
     ]
 
 
@@ -112,14 +116,14 @@ class LmpcSynthCfg(ctypes.Structure):
 class LmpcCommand(ctypes.Structure):
     _fields_ = [
         ("state", LmpcStateIn),
-        ("gait_phase", ctypes.c_double),
+        ("gait_phase", ctypes.c_double * 4),  # per leg (ABI 7)
         ("gait_speed", ctypes.c_double),
         ("gait", ctypes.c_int32),
         ("plan_contacts", ctypes.c_uint8 * 4),
     ]
 
 
-COMMAND_BYTES = ctypes.sizeof(LmpcCommand)  # 384
+COMMAND_BYTES = ctypes.sizeof(LmpcCommand)  # 408
 
 
 class LmpcLegKin(ctypes.Structure):
@@ -212,6 +216,10 @@ def lib():
         L.lmpc_current_contact.restype = ctypes.c_int
         L.lmpc_contact_schedule.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, u8p, u8p]
         L.lmpc_contact_schedule.restype = ctypes.c_int
+        if hasattr(L, "lmpc_contact_schedule_legs"):  # ABI 7 (absent from a one-ABI-behind diagnostic build)
+            L.lmpc_contact_schedule_legs.argtypes = [ctypes.c_int, dp, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                                     u8p, u8p]
+            L.lmpc_contact_schedule_legs.restype = ctypes.c_int
         L.lmpc_pack_record.argtypes = [pp, ctypes.c_int, ctypes.POINTER(LmpcStateIn), dp, dp]
         L.lmpc_pack_record.restype = ctypes.c_int
         L.lmpc_synth_cfg_go1.argtypes = [ctypes.POINTER(LmpcSynthCfg)]
@@ -285,7 +293,10 @@ def lib():
         L.lmpc_wbc_tasks.restype = ctypes.c_int
         L.lmpc_wbc_tasks_device.argtypes = [vp, ctypes.c_int, vp, vp]
         L.lmpc_wbc_tasks_device.restype = ctypes.c_int
-        if L.lmpc_abi_version() != ABI_VERSION:
+        # a diagnostic build of the previous round's sources (tools/ab_bench.sh A/B against it) may be one ABI behind:
+        # the bench path it runs (device commands, records, solve) does not depend on the ABI-7 layouts
+        ok = (ABI_VERSION - 1, ABI_VERSION) if os.environ.get("LMPC_LIB") else (ABI_VERSION,)
+        if L.lmpc_abi_version() not in ok:
             raise NativeLibraryError("liblmpc.so ABI version mismatch")
         _lib = L
         return L

@@ -48,13 +48,17 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile_lib(out: str, objdir: str, defines=(), flags=(), verbose: bool = False) -> str:
+def _compile_lib(out: str, objdir: str, defines=(), flags=(), verbose: bool = False, only=None) -> str:
     """liblmpc from SOURCES: one compile per source (HIP_FLAGS + that file's SCHED_FLAGS + `flags`, -D`defines`),
-    run in parallel, then one link; written to `out` atomically."""
+    run in parallel, then one link; written to `out` atomically.  `only`: compile just these sources and link the
+    product's objects (lib/obj, built first) for the rest."""
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     procs, objs = [], []
     for s in SOURCES:
+        if only is not None and s not in only:
+            objs.append(os.path.join(LIBDIR, "obj", s + ".o"))
+            continue
         obj = os.path.join(objdir, s + ".o")
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
                "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj] + HIP_FLAGS + \
@@ -121,6 +125,32 @@ def build_variant(tag: str, defines, force: bool = False, flags=()) -> str:
     if not force and not _stale(out, srcs + [os.path.join(CSRC, h) for h in HEADERS]):
         return out
     return _compile_lib(out, os.path.join(ROOT, "tools", "build", f"obj_{tag}"), defines=defines, flags=flags)
+
+
+TEST_BUILD = os.path.join(ROOT, "tests", "build")
+# Test-only library variants (tests/test_gpu_kkt.py), never the product: bugs re-injected into the LDS Riccati
+# kernel's forward sweep -- round 4's lost "+ za", and the next stage's yaw read for A_k -- with the polish's KKT
+# certificate (the product's verification) and without it (LMPC_KKT_OFF: round 4's verification).
+TEST_VARIANTS = {
+    "bugza": (["LMPC_BUG_ZA"], ("lmpc_lq.hip",)),
+    "bugza_nokkt": (["LMPC_BUG_ZA", "LMPC_KKT_OFF"], ("lmpc_lq.hip",)),
+    "bugyaw": (["LMPC_BUG_YAW"], ("lmpc_lq.hip",)),
+    "bugyaw_nokkt": (["LMPC_BUG_YAW", "LMPC_KKT_OFF"], ("lmpc_lq.hip",)),
+}
+
+
+def build_test_variants(force: bool = False) -> dict:
+    """The TEST_VARIANTS libraries under tests/build/ (only the named sources recompiled; the rest are the product's
+    objects, so build_native() first)."""
+    build_native()
+    out = {}
+    for tag, (defines, only) in TEST_VARIANTS.items():
+        path = os.path.join(TEST_BUILD, f"liblmpc_{tag}.so")
+        deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS] + [LIB]
+        if force or _stale(path, deps):
+            _compile_lib(path, os.path.join(TEST_BUILD, f"obj_{tag}"), defines=defines, only=only)
+        out[tag] = path
+    return out
 
 
 def build_cpp_test(force: bool = False) -> str:

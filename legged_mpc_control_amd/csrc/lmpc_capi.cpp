@@ -89,6 +89,7 @@ void fill_options(lmpc::DevParams& d, const lmpc_options* o) {
     d.dense_iter_cap = o->dense_iter_cap > 0 ? o->dense_iter_cap : (1 << 30);  // 0: never hand over
     d.dense_polish_iter = o->dense_polish_iter;
     d.warm_rounds = o->warm_rounds;
+    d.tol_x = o->tol_x;
 }
 
 bool params_ok(const lmpc_params* p) {
@@ -288,7 +289,7 @@ void lmpc_destroy(lmpc_ctx* c) {
 
 int lmpc_set_options(lmpc_ctx* c, const lmpc_options* o) {
     if (!c || !o || o->max_iter < 1 || o->max_rounds < 1 || o->max_attempts < 1 || !(o->tol_mu > 0.0) ||
-        !(o->tol_p >= 0.0) || !(o->tol_d >= 0.0) || o->gi_max_steps < 1 || o->dense_iter_cap < 0 ||
+        !(o->tol_p >= 0.0) || !(o->tol_d >= 0.0) || !(o->tol_x >= 0.0) || o->gi_max_steps < 1 || o->dense_iter_cap < 0 ||
         o->dense_polish_iter < 1 || o->warm_rounds < 1)
         return LMPC_ERR_ARG;
     fill_options(c->prm, o);

@@ -25,7 +25,7 @@
 // first statement of every function body below that does arithmetic: no a*b+c fusion in this block
 #define LMPC_NO_FMA _Pragma("clang fp contract(off)")
 
-static_assert(sizeof(lmpc_command) == 384, "lmpc_command layout (mirrored by _native.LmpcCommand)");
+static_assert(sizeof(lmpc_command) == 408, "lmpc_command layout (mirrored by _native.LmpcCommand)");
 
 namespace lmpc_common {
 
@@ -79,11 +79,12 @@ LMPC_HD inline int current_contact(int gait, int leg, double gait_phase) {
     return t.state[t.size - 1];
 }
 
-// contact[i][j] of the bound schedule (ConvexQPSolver.cpp:329-346)
+// contact[i][j] of the bound schedule (ConvexQPSolver.cpp:329-346): leg j predicted from its own FSM's phase
+// (ConvexQPSolver.cpp:341-342, LeggedContactFSM.h:64)
 LMPC_HD inline uint8_t contact_element(const lmpc_command& c, double dt, int i, int j) {
     LMPC_NO_FMA
     if (i == 0) return c.plan_contacts[j] ? 1 : 0;
-    return (uint8_t)predict_contact(c.gait, j, c.gait_phase, c.gait_speed, i * dt);
+    return (uint8_t)predict_contact(c.gait, j, c.gait_phase[j], c.gait_speed, i * dt);
 }
 
 // root_lin_vel_d_world = root_rot_mat * root_lin_vel_d_rel, component r (ConvexQPSolver.cpp:260)
@@ -199,7 +200,7 @@ LMPC_HD inline void synth_command(const lmpc_synth_cfg& cfg, uint64_t seed, uint
         st.root_euler[k] = st.root_pos[k] = st.root_ang_vel[k] = st.root_lin_vel[k] = 0.0;
         st.root_euler_d[k] = st.root_pos_d[k] = st.root_lin_vel_d_rel[k] = st.root_ang_vel_d_rel[k] = 0.0;
     }
-    c.gait_phase = 0.0;
+    for (int j = 0; j < 4; ++j) c.gait_phase[j] = 0.0;
     c.gait_speed = cfg.gait_speed;
     c.gait = cfg.gait < 0 ? LMPC_GAIT_TROT : cfg.gait;
     for (int j = 0; j < 4; ++j) c.plan_contacts[j] = 1;
@@ -238,9 +239,11 @@ LMPC_HD inline void synth_command(const lmpc_synth_cfg& cfg, uint64_t seed, uint
         for (int r = 0; r < 3; ++r)
             st.foot_pos_abs[3 * j + r] = R[3 * r] * rel[0] + R[3 * r + 1] * rel[1] + R[3 * r + 2] * rel[2];
     }
-    c.gait_phase = rng.uniform();
+    // one phase for the four legs (the FSMs of a synthetic instance are in step: no early touchdowns)
+    const double ph = rng.uniform();
+    for (int j = 0; j < 4; ++j) c.gait_phase[j] = ph;
     if (cfg.gait < 0) c.gait = (int)(rng.uniform() * 4.0) & 3;
-    for (int j = 0; j < 4; ++j) c.plan_contacts[j] = (uint8_t)current_contact(c.gait, j, c.gait_phase);
+    for (int j = 0; j < 4; ++j) c.plan_contacts[j] = (uint8_t)current_contact(c.gait, j, c.gait_phase[j]);
 }
 
 // Terrain normals of instance `index`, leg j (own Philox stream "TERR")

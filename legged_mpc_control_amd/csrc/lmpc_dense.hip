@@ -55,6 +55,20 @@ __device__ unsigned long long lmpc_dense_stamps[4096][DSTAMP_N];
 #define DSTAMP_FLUSH(qp) do {} while (0)
 #endif
 
+#ifdef LMPC_KKT_DIAG
+// diagnostic build (tools/kkt_diag.py): per QP, at its last settled polish round, stationarity residual / gscale
+__device__ double lmpc_kkt_diag_dense[LMPC_KKT_DIAG_QPS][4];
+extern "C" int lmpc_debug_kkt_dense(double* out, int nqp) {
+    if (nqp > LMPC_KKT_DIAG_QPS) nqp = LMPC_KKT_DIAG_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_kkt_diag_dense), (size_t)nqp * 4 * sizeof(double)) == hipSuccess
+               ? nqp : -1;
+}
+extern "C" int lmpc_debug_kkt_dense_clear(void) {
+    static double zeros[LMPC_KKT_DIAG_QPS * 4];
+    return hipMemcpyToSymbol(HIP_SYMBOL(lmpc_kkt_diag_dense), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // The dense-path kernel.  One wave per QP; QPs with more than 20 stance leg-steps are left to the
 // Riccati kernel (lmpc_qp_kernel), which skips the ones handled here.
@@ -504,6 +518,7 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
             }
             const double gscale = wave_max(gloc);
             int changed = 0;
+            double sres = 0.0;  // stationarity residual on the leg-step's free directions (lmpc_kernel_common.h)
             if (st) {
                 double o[5];
                 cons_resid(u, mu, fzmax, o);
@@ -518,26 +533,44 @@ __global__ void __launch_bounds__(64) lmpc_dense_kernel(const DevParams prm, con
                 if (imax >= 0) {
                     act |= 1 << imax;
                     changed = 1;
-                } else if (apex) {
+                } else if (apex) {  // the cone test is the whole certificate at the apex
                     if (g[2] / mu < fabs(g[0]) + fabs(g[1]) - prm.tol_d * gscale) {
                         act = (g[0] < 0.0 ? 2 : 1) | (g[1] < 0.0 ? 8 : 4);
                         changed = 1;
                     }
-                } else if (act != 0) {
-                    const int df = leg_drop_face(act, g, mu, -prm.tol_d * gscale);
-                    if (df >= 0) {
-                        act &= ~(1 << df);
+                } else {  // (act = 0: no multipliers, the residual is g itself)
+                    const LegKkt kk = leg_kkt(act, g, mu, -prm.tol_d * gscale);
+                    if (kk.drop >= 0) {
+                        act &= ~(1 << kk.drop);
                         changed = 1;
                     }
+                    sres = kk.res;
                 }
             }
             DSTAMP(10);  // polish verification
             const unsigned long long chg = __ballot(changed);
             if (!chg) {
-                done = true;
-                break;
+                // a settled active set is the optimum's only if H u + g vanishes on every free direction; otherwise
+                // this attempt cannot verify (another round would repeat it) and the retry ladder takes over
+                const double sr = wave_max(sres);
+#ifdef LMPC_KKT_DIAG
+                if (lane == 0 && qp < LMPC_KKT_DIAG_QPS) {
+                    lmpc_kkt_diag_dense[qp][0] = sr / gscale;
+                    lmpc_kkt_diag_dense[qp][1] = 0.0;
+                    lmpc_kkt_diag_dense[qp][2] = gscale;
+                    lmpc_kkt_diag_dense[qp][3] = 1.0;
+                }
+#endif
+#ifndef LMPC_KKT_OFF
+                if (sr <= prm.tol_d * gscale)
+#endif
+                {
+                    done = true;
+                    break;
+                }
+                rd = prm.max_rounds - 1;
             }
-            keep_tiles = (__ffsll((long long)chg) - 1) / 5;  // tile of the first changed leg-step
+            keep_tiles = chg ? (__ffsll((long long)chg) - 1) / 5 : 0;  // tile of the first changed leg-step
             if (++rd >= prm.max_rounds) {
                 keep_tiles = 0;
                 if (++att >= prm.max_attempts) break;

@@ -18,10 +18,11 @@ struct DevParams {
     double tol_mu;     // IPM stop: mean complementarity
     double tol_p;      // polish primal tolerance (relative to fmax)
     double tol_d;      // polish dual tolerance (relative to gradient scale)
+    double tol_x;      // polish certificate: trajectory vs the forces' dynamics (relative to the state scale)
     int H;             // horizon
     int max_iter;      // IPM iteration cap (per attempt)
     int max_rounds;    // polish rounds per attempt
-    int max_attempts;  // IPM+polish attempts (tol_mu tightened x1e-3 per attempt)
+    int max_attempts;  // IPM+polish attempts (the stop tightened per attempt: retry_tol, lmpc_kernel_common.h)
     int dense;         // QPs with 1..DENSE_MAX_LS stance leg-steps: 0 Riccati kernel, 1 condensed interior
                        // point (lmpc_dense.hip), 2 condensed dual active set (lmpc_gi.hip)
     int gi_max_steps;  // dual active-set step cap; a QP that reaches it is solved by the Riccati kernel

@@ -46,6 +46,16 @@ __device__ unsigned long long lmpc_gi_stamps[4096][8];
 #define GSTAMP_FLUSH(qp) do {} while (0)
 #endif
 
+#ifdef LMPC_KKT_DIAG
+// diagnostic build (tools/kkt_diag.py): per QP, the certificate's stationarity residual / gscale and its verdict
+__device__ double lmpc_kkt_diag_gi[LMPC_KKT_DIAG_QPS][4];
+extern "C" int lmpc_debug_kkt_gi(double* out, int nqp) {
+    if (nqp > LMPC_KKT_DIAG_QPS) nqp = LMPC_KKT_DIAG_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_kkt_diag_gi), (size_t)nqp * 4 * sizeof(double)) == hipSuccess ? nqp
+                                                                                                                 : -1;
+}
+#endif
+
 constexpr int GI_EXTRA = 3 * 64 + 3 * 64 + 2 * 64;  // LDS doubles ahead of the DSmem area
 
 struct GSmem {
@@ -591,6 +601,64 @@ __global__ void __launch_bounds__(64) lmpc_gi_kernel(const DevParams prm, const 
         if (lane == 0) done[qp] = 0;  // the Riccati kernel solves this QP
         GSTAMP_FLUSH(qp);
         return;
+    }
+    // ---- KKT certificate, independent of the active-set algebra (J, R^-1, the multipliers uu): the gradient
+    //      H x + g from the condensed QP itself (its tiles and g rebuilt: R^-1 overwrote them), then per stance
+    //      leg-step primal feasibility, the least-squares multipliers of its active faces (sign) and the stationarity
+    //      residual on its free directions; the apex by the cone test.  A QP that fails it is left to the Riccati
+    //      kernel, like one that hits the step cap ----
+    {
+        LMPC_SYNC();
+        dense_condense<TERRAIN>(prm, S, H, nls, smask, lane);
+        S.vec2[lane] = xv;
+        LMPC_SYNC();
+        const double gl = h_matvec(S, S.vec2, S.scr, lane) + S.gv[lane];
+        LMPC_SYNC();
+        S.vec[lane] = gl;
+        LMPC_SYNC();
+        double g[3] = {0.0, 0.0, 0.0}, u[3] = {0.0, 0.0, 0.0};
+        double gloc = 1.0;
+        if (lane < nls) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                g[p] = S.vec[lv0 + p];
+                u[p] = S.vec2[lv0 + p];
+                gloc = fmax(gloc, fabs(g[p]));
+            }
+        }
+        const double gscale = wave_max(gloc);
+        double sres = 0.0;
+        bool fail = false;
+        if (lane < nls) {
+            double o[5];
+            cons_resid(u, mu, fzmax, o);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) fail |= o[i] > prm.tol_p * fzmax;
+            if ((lact & 3) == 3 || (lact & 12) == 12) {  // apex (f = 0): the cone test
+                fail |= g[2] / mu < fabs(g[0]) + fabs(g[1]) - prm.tol_d * gscale;
+            } else {
+                const LegKkt kk = leg_kkt(lact, g, mu, -prm.tol_d * gscale);
+                fail |= kk.drop >= 0;
+                sres = kk.res;
+            }
+        }
+        const double sr = wave_max(sres);
+#ifdef LMPC_KKT_DIAG
+        if (lane == 0 && qp < LMPC_KKT_DIAG_QPS) {
+            lmpc_kkt_diag_gi[qp][0] = sr / gscale;
+            lmpc_kkt_diag_gi[qp][1] = __any(fail) ? 1.0 : 0.0;
+            lmpc_kkt_diag_gi[qp][2] = gscale;
+            lmpc_kkt_diag_gi[qp][3] = 1.0;
+        }
+#endif
+#ifndef LMPC_KKT_OFF
+        if (__any(fail) || !(sr <= prm.tol_d * gscale)) {
+            if (lane == 0) done[qp] = 0;  // the Riccati kernel solves this QP
+            GSTAMP_FLUSH(qp);
+            return;
+        }
+#endif
+        LMPC_SYNC();
     }
     // ---- output: stance forces through LDS to the lane of leg-step 4k + j ----
     S.vec[lane] = xv;

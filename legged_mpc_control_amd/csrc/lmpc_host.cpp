@@ -56,6 +56,9 @@ void lmpc_options_default(lmpc_options* o) {
     o->dense_iter_cap = 0;
     o->dense_polish_iter = 40;  // = max_iter: the polish only once the interior point has converged
     o->warm_rounds = 12;        // tools/tick_latency sweep: 4 -> 0.59 ms, 12 -> 0.35 ms per tick at H = 30
+    // the certificate's dynamics check: its rounding level is <= 2e-10 of the state scale over configs 2-5 (reduced-input
+    // polish stages whose W pivots sit near 1e-6 of their diagonal; tools/kkt_diag.py), a real inconsistency is O(1)
+    o->tol_x = 1e-8;
 }
 
 int lmpc_record_len(int horizon) { return 33 + 12 * horizon; }
@@ -88,6 +91,16 @@ int lmpc_contact_schedule(int gait, double gait_phase, double gait_speed, double
     for (int i = 1; i < horizon; ++i)
         for (int j = 0; j < 4; ++j)
             contact[4 * i + j] = (uint8_t)lmpc_predict_contact(gait, j, gait_phase, gait_speed, i * dt);
+    return LMPC_OK;
+}
+
+int lmpc_contact_schedule_legs(int gait, const double gait_phase[4], double gait_speed, double dt, int horizon,
+                               const uint8_t plan_contacts[4], uint8_t* contact) {
+    if (horizon < 1 || !gait_phase || !plan_contacts || !contact) return LMPC_ERR_ARG;
+    for (int j = 0; j < 4; ++j) contact[j] = plan_contacts[j] ? 1 : 0;
+    for (int i = 1; i < horizon; ++i)
+        for (int j = 0; j < 4; ++j)
+            contact[4 * i + j] = (uint8_t)lmpc_predict_contact(gait, j, gait_phase[j], gait_speed, i * dt);
     return LMPC_OK;
 }
 
@@ -154,8 +167,8 @@ int lmpc_command_to_record(const lmpc_params* p, int horizon, const lmpc_command
                            uint8_t* contact) {
     if (!p || !cmd || !rec || !contact || horizon < 1) return LMPC_ERR_ARG;
     lmpc_pack_record(p, horizon, &cmd->state, rec, nullptr);
-    return lmpc_contact_schedule(cmd->gait, cmd->gait_phase, cmd->gait_speed, p->dt, horizon, cmd->plan_contacts,
-                                 contact);
+    return lmpc_contact_schedule_legs(cmd->gait, cmd->gait_phase, cmd->gait_speed, p->dt, horizon, cmd->plan_contacts,
+                                      contact);
 }
 
 int lmpc_synth_commands(const lmpc_synth_cfg* cfg, uint64_t seed, int64_t first_index, int count, lmpc_command* cmd) {

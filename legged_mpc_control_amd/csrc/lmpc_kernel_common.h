@@ -34,6 +34,10 @@ constexpr int LMPC_WAVE = 64;
 #ifndef LMPC_ACT_RATIO
 #define LMPC_ACT_RATIO 1e-3
 #endif
+// diagnostic builds only (-DLMPC_KKT_DIAG): per-QP certificate residuals kept for this many QPs per kernel
+#ifdef LMPC_KKT_DIAG
+#define LMPC_KKT_DIAG_QPS 65536
+#endif
 #define LMPC_SYNC()                                              \
     do {                                                         \
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
@@ -266,10 +270,75 @@ __device__ __forceinline__ bool leg_basis(int act, double mu, double fzmax, doub
     return false;
 }
 
-// Polish verification of one (non-apex) leg-step: multipliers of its active faces from
-// C_S' z = -g (C_S = the <= 3 active rows, full row rank), by Gaussian elimination on the Gram
-// matrix C_S C_S' padded to 3x3 with identity rows.  Returns the face whose multiplier is the most
-// negative below zmin (the one to drop), or -1.
+// KKT certificate of one (non-apex) stance leg-step with active faces `act` (ConvexQPSolver.cpp:131-172 rows) at the
+// gradient g = dJ/df of the leg's force: the least-squares multipliers z of C_S' z = -g (C_S = the <= 3 active rows,
+// full row rank; none when act = 0), by Gaussian elimination on the Gram matrix C_S C_S' padded to 3x3 with
+// identity rows.  `drop`: the face whose multiplier is the most negative below zmin (the one to drop), or -1.
+// `res`: the stationarity residual |g + C_S' z|_inf -- the part of g on the leg's free directions (the null space of
+// C_S), which the polish's equality-constrained solve makes zero: a verified active set must also have res at
+// rounding level, or the returned forces are not the optimum whatever the multiplier signs say.
+struct LegKkt {
+    int drop;
+    double res;
+};
+__device__ __forceinline__ LegKkt leg_kkt(int act, const double g[3], double mu, double zmin) {
+    const ActiveRows ar = active_rows(act);
+    const int nr = ar.nr;
+    double C[3][3];
+    cons_rowvec(ar.i0, mu, C[0]);
+    cons_rowvec(ar.i1, mu, C[1]);
+    cons_rowvec(ar.i2, mu, C[2]);
+    double Gm[3][3], rhs[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        rhs[a] = a < nr ? -(C[a][0] * g[0] + C[a][1] * g[1] + C[a][2] * g[2]) : 0.0;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const double v = C[a][0] * C[b][0] + C[a][1] * C[b][1] + C[a][2] * C[b][2];
+            Gm[a][b] = (a < nr && b < nr) ? v : (a == b ? 1.0 : 0.0);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int b = a + 1; b < 3; ++b) {
+            const double fct = Gm[b][a] / Gm[a][a];
+#pragma unroll
+            for (int c = a; c < 3; ++c) Gm[b][c] -= fct * Gm[a][c];
+            rhs[b] -= fct * rhs[a];
+        }
+    }
+    double zz[3];
+#pragma unroll
+    for (int a = 2; a >= 0; --a) {
+        double v = rhs[a];
+#pragma unroll
+        for (int b = a + 1; b < 3; ++b) v -= Gm[a][b] * zz[b];
+        zz[a] = v / Gm[a][a];
+    }
+    LegKkt o;
+    o.drop = -1;
+    double zm = zmin;
+    const int fi[3] = {ar.i0, ar.i1, ar.i2};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        if (a < nr && zz[a] < zm) {
+            zm = zz[a];
+            o.drop = fi[a];
+        }
+    // r = g + C_S' z (slots beyond nr carry z = 0 from the padded rows)
+    o.res = 0.0;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        double r = g[p];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) r += (a < nr ? zz[a] : 0.0) * C[a][p];
+        o.res = fmax(o.res, fabs(r));
+    }
+    return o;
+}
+
+// Polish verification of one (non-apex) leg-step: the face to drop (leg_kkt without the residual).
 __device__ __forceinline__ int leg_drop_face(int act, const double g[3], double mu, double zmin) {
     const ActiveRows ar = active_rows(act);
     const int nr = ar.nr;

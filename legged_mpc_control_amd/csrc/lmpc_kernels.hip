@@ -1300,8 +1300,45 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                 mode = PRED;
                 SUB(18);  // (diagnostic) corrector post-step
             } else {
-                // ---- polish verification: primal feasibility + multiplier signs ----
+                // ---- polish verification, a KKT certificate independent of the factorisation (lmpc_lq.hip): the
+                // trajectory is the dynamics of the forces returned, the adjoint of that trajectory gives the
+                // gradient, every stance leg-step is primal feasible, stationary on its free directions and carries
+                // multipliers of the right sign ----
                 STAMP(1);
+                double dres = 0.0, xsc = 1.0;  // dynamics residual, state scale (max |x|, at least 1)
+                {
+                    // B u_k per stage -> SO_N6 (dead after the solve)
+#pragma unroll
+                    for (int t = 0; t < LS; ++t) {
+                        const int j = lsj[t];
+                        double bu[6];
+#pragma unroll
+                        for (int m = 0; m < 6; ++m)
+                            bu[m] = quad_sum(fma(S.G0[m * 12 + 3 * j], u[t][0],
+                                                 fma(S.G0[m * 12 + 3 * j + 1], u[t][1], S.G0[m * 12 + 3 * j + 2] * u[t][2])));
+                        if (valid[t] && j == 0) {
+#pragma unroll
+                            for (int m = 0; m < 6; ++m) S.st[lsk[t] * SK + SO_N6 + m] = bu[m];
+                        }
+                    }
+                    LMPC_SYNC();
+                    constexpr int MAXT = (12 * LMPC_MAX_HORIZON + 63) / 64;
+#pragma unroll 1
+                    for (int i = 0; i < MAXT; ++i) {
+                        if (64 * i >= 12 * H) break;  // wave-uniform
+                        const int e = lane + 64 * i, ec = e < 12 * H ? e : 12 * H - 1;
+                        const int k = ec / 12, r = ec - 12 * k;
+                        const ldouble* xk = S.st + k * SK + SO_XS;
+                        const double xn = k + 1 < H ? S.st[(k + 1) * SK + SO_XS + r] : S.xH[r];
+                        const int m = r >= 6 ? r - 6 : 0;
+                        const double bu = S.st[k * SK + SO_N6 + m] - (m == 5 ? prm.grav * dt : 0.0);
+                        const double pred = Ax_el(xk, r, S.cs[2 * k], S.cs[2 * k + 1], dt) + (r >= 6 ? bu : 0.0);
+                        if (e < 12 * H) {
+                            dres = fmax(dres, fabs(xn - pred));
+                            xsc = fmax(xsc, fabs(xn));
+                        }
+                    }
+                }
                 adjoint(prm, S, lane);
                 STAMP(4);  // adjoint
                 double g[LS][3];
@@ -1333,6 +1370,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                 }
                 const double gscale = wave_max(gloc);
                 int changed = 0;
+                double sres = 0.0;  // stationarity residual on the free directions of the stance leg-steps
 #pragma unroll
                 for (int t = 0; t < LS; ++t) {
                     if (!st[t]) continue;
@@ -1351,27 +1389,36 @@ __global__ void __launch_bounds__(64, WPE) lmpc_qp_kernel(const DevParams prm, c
                         changed = 1;
                         continue;
                     }
-                    if (apex[t]) {
+                    if (apex[t]) {  // the cone test is the whole certificate at the apex
                         if (g[t][2] / mu < fabs(g[t][0]) + fabs(g[t][1]) - prm.tol_d * gscale) {
                             act[t] = (g[t][0] < 0.0 ? 2 : 1) | (g[t][1] < 0.0 ? 8 : 4);
                             changed = 1;
                         }
                         continue;
                     }
-                    if (act[t] == 0) continue;
-                    // multipliers: C_S' z = -g, C_S full row rank (<= 3 rows)
-                    const int df = leg_drop_face(act[t], g[t], mu, -prm.tol_d * gscale);
-                    if (df >= 0) {
-                        act[t] &= ~(1 << df);
+                    // multipliers: C_S' z = -g, C_S full row rank (<= 3 rows; act = 0: none, the residual is g)
+                    const LegKkt kk = leg_kkt(act[t], g[t], mu, -prm.tol_d * gscale);
+                    if (kk.drop >= 0) {
+                        act[t] &= ~(1 << kk.drop);
                         changed = 1;
                     }
+                    sres = fmax(sres, kk.res);
                 }
+                bool settled = false;  // the active set no longer changes, but the certificate failed
                 if (!__any(changed)) {
-                    done = true;
+                    const double sr = wave_max(sres), dr = wave_max(dres), xs = wave_max(xsc);
+#ifndef LMPC_KKT_OFF
+                    if (sr <= prm.tol_d * gscale && dr <= prm.tol_x * xs)
+#endif
+                    {
+                        done = true;
 #pragma unroll
-                    for (int t = 0; t < LS; ++t) act_fin[t] = st[t] ? act[t] : 0;
-                    break;
+                        for (int t = 0; t < LS; ++t) act_fin[t] = st[t] ? act[t] : 0;
+                        break;
+                    }
+                    settled = true;  // another round would repeat it bit for bit: the retry ladder takes over
                 }
+                if (settled) rd = (warm ? prm.warm_rounds : prm.max_rounds) - 1;
                 if (++rd >= (warm ? prm.warm_rounds : prm.max_rounds)) {
                     if (warm) {  // the warm active set did not verify: the cold interior point
                         warm = false;

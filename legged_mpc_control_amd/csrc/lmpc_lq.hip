@@ -62,6 +62,20 @@ __device__ unsigned long long lmpc_lq_stamps[LQ_STAMP_QPS][LQ_STAMP_N];
 #define LQ_STAMP_FLUSH(qp) do {} while (0)
 #endif
 
+#ifdef LMPC_KKT_DIAG
+// diagnostic build (tools/kkt_diag.py): per QP, at its last settled polish round, the stationarity residual / gscale,
+// the dynamics residual / state scale, gscale and the state scale
+__device__ double lmpc_kkt_diag[LMPC_KKT_DIAG_QPS][4];
+extern "C" int lmpc_debug_kkt_lq(double* out, int nqp) {
+    if (nqp > LMPC_KKT_DIAG_QPS) nqp = LMPC_KKT_DIAG_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_kkt_diag), (size_t)nqp * 4 * sizeof(double)) == hipSuccess ? nqp : -1;
+}
+extern "C" int lmpc_debug_kkt_lq_clear(void) {
+    static double zeros[LMPC_KKT_DIAG_QPS * 4];
+    return hipMemcpyToSymbol(HIP_SYMBOL(lmpc_kkt_diag), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #ifdef LMPC_LQ_DEBUG
 __device__ double lmpc_lq_dbg[8192];
 __device__ double lmpc_lq_dbg_u[384];
@@ -376,6 +390,10 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
         const double mc = 5.0 * nst;
         double tol = prm.tol_mu;
         int att = 0, rd = 0, it_end = prm.max_iter, mode = PRED;
+        // the polish's reduced-input stages switched off for the rest of this QP (wave-uniform): set when a settled
+        // active set fails the certificate's dynamics check -- a nearly rank-deficient W_k whose tiny directions the
+        // reduced stage drops leaves the swept trajectory off the forces' own (2 of 65536 flat config-4 QPs, 1e-6)
+        bool rp_off = false;
         int act[LS];
         bool apex[LS];
 #pragma unroll
@@ -771,7 +789,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         }
 #pragma unroll
                         for (int e = 0; e < 21; ++e) wz[e] = w[e];
-                        if (!red) ex[k] = wellc ? 1.0 : 0.0;
+                        if (!red) ex[k] = (wellc && !rp_off) ? 1.0 : 0.0;
                     }
                     LMPC_SYNC();
                 }
@@ -1123,8 +1141,17 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     #pragma unroll
                         for (int i = 0; i < 3; ++i) o.kz[i] = kzr[k * 72 + a * 12 + 3 * part + i];
                         o.c = sl[LQ_DV + a] - sl[LQ_RHO + a];
-                        o.ck = cs[2 * k];
-                        o.sk = cs[2 * k + 1];
+#ifdef LMPC_BUG_ZA  // diagnostic variant: the same lost "+ za" here, t = K za + rho without K za
+    #pragma unroll
+                        for (int n = 0; n < 6; ++n) o.c += sl[LQ_K + pk6(a, n)] * sl[LQ_Z + n * 13 + 12];
+#endif
+#ifdef LMPC_BUG_YAW  // diagnostic variant (tests/test_gpu_kkt.py): the forward sweep reads the next stage's yaw
+                        const int ky = k + 1 < H ? k + 1 : k;
+#else
+                        const int ky = k;
+#endif
+                        o.ck = cs[2 * ky];
+                        o.sk = cs[2 * ky + 1];
                     };
                     KzOps cur, nxt;
                     load(0, cur);
@@ -1174,8 +1201,13 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         o.za = sl[LQ_Z + m * 13 + 12];
     #pragma unroll
                         for (int i = 0; i < 3; ++i) o.z[i] = sl[LQ_Z + m * 13 + 3 * part + i];
-                        o.ck = cs[2 * k];
-                        o.sk = cs[2 * k + 1];
+#ifdef LMPC_BUG_YAW
+                        const int ky = k + 1 < H ? k + 1 : k;
+#else
+                        const int ky = k;
+#endif
+                        o.ck = cs[2 * ky];
+                        o.sk = cs[2 * ky + 1];
                     };
                     FwOps cur, nxt;
                     load(0, cur);
@@ -1192,7 +1224,11 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         w = fma(cur.z[1], x[3 * part + 1], w);
                         w = fma(cur.z[2], x[3 * part + 2], w);
                         const double xa = lq_row_apply(x, r, lq_ax_row(r, cur.ck, cur.sk), dt);
+#ifdef LMPC_BUG_ZA  // diagnostic variant (tests/test_gpu_kkt.py): round 4's lost "+ za", w = Z x
+                        w = quad_sum(w);
+#else
                         w = quad_sum(w) + cur.za;
+#endif
                         // w_m to every lane (readlane in uniform control flow: all lanes take part in the DPP sums
                         // above, and the broadcast reads lanes 0, 4, ..., 20)
                         double wb[6];
@@ -1362,8 +1398,58 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 LQ_STAMP(7);  // corrector step
             } else {
                 ++prounds;
-                // ======== polish verification: the adjoint lambda from the trajectory (independent of the
-                // factorisation), then primal feasibility and multiplier signs (lmpc_kernels.hip) ========
+                // ======== polish verification, a KKT certificate independent of the factorisation: the trajectory
+                // the forward sweep produced must be the dynamics of the forces returned (x_{k+1} = A_k x_k + B u_k -
+                // g dt e11, every row at once), the adjoint lambda of that trajectory gives the gradient, and every
+                // stance leg-step must then be primal feasible, stationary on its free directions and carry
+                // multipliers of the right sign (lmpc_kernels.hip) ========
+                bool dyn_ok;  // wave-uniform: the dynamics residual within tol_p of the state scale (max |x|, >= 1)
+#ifdef LMPC_KKT_DIAG
+                double lmpc_kkt_dyn;
+#endif
+                {
+                    // B u_k per stage (rows 6-11: G0 u_k, summed over the stage's legs) -> the dv field, dead until
+                    // the next leg-step work rewrites it
+#pragma unroll
+                    for (int t = 0; t < LS; ++t) {
+                        const int j = lsj[t];
+                        double bu[6];
+#pragma unroll
+                        for (int m = 0; m < 6; ++m)
+                            bu[m] = quad_sum(fma(G0s[m * 12 + 3 * j], u[t][0],
+                                                 fma(G0s[m * 12 + 3 * j + 1], u[t][1], G0s[m * 12 + 3 * j + 2] * u[t][2])));
+                        if (valid[t] && j == 0) {
+#pragma unroll
+                            for (int m = 0; m < 6; ++m) slots[lsk[t] * LQ_SLOT + LQ_DV + m] = bu[m];
+                        }
+                    }
+                    LMPC_SYNC();
+                    // every dynamics row at once: x_{j+1} - (A_j x_j + B u_j - g dt e11), x_0 from the record
+                    constexpr int NTQ = LS == 1 ? 3 : 6;
+                    double dres = 0.0, xsc = 1.0;
+#pragma unroll 1  // unrolled, its loads all in flight at once push the two-leg-step instances into spills
+                    for (int i = 0; i < NTQ; ++i) {
+                        const int e = lq_lane<WPE>(lane) + 64 * i, ec = e < 12 * H ? e : 12 * H - 1;
+                        const int j = ec / 12, rr_ = ec - 12 * j;
+                        const ldouble* xk = j > 0 ? slots + (j - 1) * LQ_SLOT + LQ_X : hdr;
+                        const int m = rr_ >= 6 ? rr_ - 6 : 0;
+                        const double pred = lq_row_apply(xk, rr_, lq_ax_row(rr_, cs[2 * j], cs[2 * j + 1]), dt) +
+                                            (rr_ >= 6 ? slots[j * LQ_SLOT + LQ_DV + m] - (m == 5 ? prm.grav * dt : 0.0) : 0.0);
+                        const double xn = slots[j * LQ_SLOT + LQ_X + rr_];
+                        if (e < 12 * H) {
+                            dres = fmax(dres, fabs(xn - pred));
+                            xsc = fmax(xsc, fabs(xn));
+                        }
+                    }
+                    {
+                        const double dmax = wave_max(dres), xmax = wave_max(xsc);
+                        dyn_ok = dmax <= prm.tol_x * xmax;
+#ifdef LMPC_KKT_DIAG
+                        lmpc_kkt_dyn = dmax / xmax;
+#endif
+                    }
+                    LMPC_SYNC();  // every read of x ahead of the tracking terms over it
+                }
                 {
                     // tracking terms q (x_k - x_ref,k-1) of every stage at once -> x slot (dead after this), then the
                     // serial sweep lambda_k = q_k-term + A_k' lambda_{k+1}, lambda_{k+1}[6:12] -> rho slot k
@@ -1426,6 +1512,7 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                 }
                 const double gscale = wave_max(gloc);
                 int changed = 0;
+                double sres = 0.0;  // stationarity residual on the free directions of the stance leg-steps
 #pragma unroll
                 for (int t = 0; t < LS; ++t) {
                     if (!st[t]) continue;
@@ -1444,24 +1531,47 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
                         changed = 1;
                         continue;
                     }
-                    if (apex[t]) {
+                    if (apex[t]) {  // the cone test is the whole certificate at the apex (f = 0, every direction bound)
                         if (g[t][2] / mu < fabs(g[t][0]) + fabs(g[t][1]) - prm.tol_d * gscale) {
                             act[t] = (g[t][0] < 0.0 ? 2 : 1) | (g[t][1] < 0.0 ? 8 : 4);
                             changed = 1;
                         }
                         continue;
                     }
-                    if (act[t] == 0) continue;
-                    const int df = leg_drop_face(act[t], g[t], mu, -prm.tol_d * gscale);
-                    if (df >= 0) {
-                        act[t] &= ~(1 << df);
+                    // (act = 0: no multipliers, the residual is g itself)
+                    const LegKkt kk = leg_kkt(act[t], g[t], mu, -prm.tol_d * gscale);
+                    if (kk.drop >= 0) {
+                        act[t] &= ~(1 << kk.drop);
                         changed = 1;
                     }
+                    sres = fmax(sres, kk.res);
                 }
                 LQ_STAMP(9);  // polish verification
                 if (!__any(changed)) {
-                    done = true;
-                    break;
+                    // the active set is settled: it is the optimum's only if the trajectory is the forces' own and the
+                    // gradient vanishes on every free direction; otherwise this attempt cannot verify (another round
+                    // would repeat it bit for bit) and the retry ladder takes over
+                    const double sr = wave_max(sres);
+#ifdef LMPC_KKT_DIAG
+                    if (lane == 0 && qp < LMPC_KKT_DIAG_QPS) {
+                        lmpc_kkt_diag[qp][0] = sr / gscale;
+                        lmpc_kkt_diag[qp][1] = lmpc_kkt_dyn;
+                        lmpc_kkt_diag[qp][2] = gscale;
+                        lmpc_kkt_diag[qp][3] = (double)prounds;
+                    }
+#endif
+#ifndef LMPC_KKT_OFF
+                    if (sr <= prm.tol_d * gscale && dyn_ok)
+#endif
+                    {
+                        done = true;
+                        break;
+                    }
+                    if (LQ_RP && !dyn_ok && !rp_off) {
+                        rp_off = true;  // the same active set again, every polish stage in full inputs
+                        continue;
+                    }
+                    rd = prm.max_rounds - 1;
                 }
                 if (++rd >= prm.max_rounds) {
                     if (++att >= prm.max_attempts) break;

@@ -53,7 +53,7 @@ class MultiDeviceSolver:
         check_device_tensor(name, t, dtype, shape, torch.device("cuda", self.devices[0]))
 
     def solve_commands_device(self, d_cmd, d_grf, d_status=None, d_iters=None, d_normals=None, stream=None):
-        """Commands uint8 [B, 384] on devices[0] -> GRFs [B, H, 12] (+ status, iters) on devices[0]; synchronous."""
+        """Commands uint8 [B, 408] on devices[0] -> GRFs [B, H, 12] (+ status, iters) on devices[0]; synchronous."""
         import torch
 
         B = int(d_cmd.shape[0])
@@ -88,7 +88,7 @@ class MultiDeviceSolver:
         return grf, st, it
 
     def solve_commands(self, cmd: np.ndarray, normals: np.ndarray | None = None):
-        """Host commands uint8 [B, 384] (+ normals [B, 4, 3]) -> host (grf, status, iters)."""
+        """Host commands uint8 [B, 408] (+ normals [B, 4, 3]) -> host (grf, status, iters)."""
         cmd = np.ascontiguousarray(cmd, dtype=np.uint8)
         B = cmd.shape[0]
         if cmd.shape != (B, N.COMMAND_BYTES):

@@ -49,6 +49,68 @@ def qp_flop(H: int, ipm_iters: float, polish_rounds: float) -> float:
     return ipm_iters * ipm_iter_flop(H) + polish_rounds * polish_round_flop(H)
 
 
+# ---- the LDS Riccati kernel (lmpc_lq.hip, round 4 on): useful flops of the formulation it runs -----------------
+#   Counted from the algorithm on the nonzero structure (FMA = 2 flops), not from the padded
+# 16x16 MFMA tiles or the exec-masked lanes the PMC counters see; n = 12 states, 13 with the affine column of P^,
+# m = 6 rows reached by the inputs (6-11), dt N(yaw) has 8 nonzeros.  Per horizon stage:
+#   interior-point factorisation (reduced inputs, six unit-cost inputs f = U v - g):
+#     U = chol(W) 36 + C = P^[:,6:12] [U | dv] 13 x 27 = 351 + Guu' = I + U'(P22 U) 91 + chol(Guu') 36
+#     + X = L^-1 U' 90 + K = X'X 126 + P^ dtN 104 + KZ = K Z 468 + dtN' PA 104 + PA' KZ (symmetric) 546 = 1952 FMA
+#   polish factorisation: the same in reduced inputs where W_k is well conditioned (one leg-step per lane), plus the
+#     linear term's column (13 x 6 + 6 x 6 = 114); full inputs (two leg-steps per lane: H > 16):
+#     C = P^[:,6:12] [Bt | dv] 13 x 6 x 13 = 1014 + Guu = Rr + Bt'P22 Bt 78 x 6 = 468 + block Cholesky, L^-1 and
+#     X = L^-1 [Bt' | r] 288 + 504 + KH = X'X (7 x 7) 336 + PA 104 + KZ 468 + P 650 = 3832 FMA
+#   per Newton system: forward sweep 6 x 12 + 8 = 80, costate lambda2 = Z A^-1 x' 80                  = 160 FMA
+#   corrector: P22 dg 72 + rho 36 + q' 72 + backward sweep 80 + t = K za + rho 36                     = 296 FMA
+#   polish verification: B u rows 36, dynamics rows 36, tracking 12, adjoint 20                      =  104 FMA
+# per stance leg-step:
+#   interior point, per factorisation: W, C'WC, Rr and its Cholesky, L^-1 rr, Y = G0_j L^-T, g_j, W_j = Y Y'  150 FMA
+#   polish, per factorisation: null basis, T'RbT, rr, Bt = G0 T, Y and W_j                                   260 FMA
+#   per Newton system: G0_j' lambda2, the 3 x 3 solve, the step-length terms                                  60 FMA
+#   polish verification: G0_j u, g = R u + G0_j' lambda, the multiplier fit and the stationarity residual   100 FMA
+# per stage and factorisation: the quad sums of W_j and g_j (27 entries x 3 adds)                             81 flops
+LQ_IPM_FACT_FMA = 1952
+LQ_POL_FACT_RED_FMA = 1952 + 114
+LQ_POL_FACT_FULL_FMA = 3832
+LQ_SYSTEM_FMA = 160
+LQ_CORR_FMA = 296
+LQ_VERIFY_FMA = 104
+LQ_LEG_IPM_FMA = 150
+LQ_LEG_POL_FMA = 260
+LQ_LEG_SYSTEM_FMA = 60
+LQ_LEG_VERIFY_FMA = 100
+LQ_QUAD_FLOP = 81
+
+
+def lq_flop(H: int, ipm_iters: float, polish_rounds: float, stance_per_stage: float) -> float:
+    """Useful flops of one QP on the LDS Riccati kernel given its (mean) interior-point iterations, polish rounds and
+    stance leg-steps per stage (an interior-point iteration = one factorisation + predictor and corrector systems;
+    a polish round = one factorisation + one system + the verification)."""
+    s = stance_per_stage
+    reduced_polish = 4 * H <= 64  # one leg-step per lane: reduced-input polish stages (LQ_RP)
+    ipm_stage = 2 * (LQ_IPM_FACT_FMA + 2 * LQ_SYSTEM_FMA + LQ_CORR_FMA
+                     + s * (LQ_LEG_IPM_FMA + 2 * LQ_LEG_SYSTEM_FMA)) + LQ_QUAD_FLOP
+    pol_fact = LQ_POL_FACT_RED_FMA if reduced_polish else LQ_POL_FACT_FULL_FMA
+    pol_stage = 2 * (pol_fact + LQ_SYSTEM_FMA + LQ_VERIFY_FMA
+                     + s * (LQ_LEG_POL_FMA + LQ_LEG_SYSTEM_FMA + LQ_LEG_VERIFY_FMA)) + LQ_QUAD_FLOP
+    return H * (ipm_iters * ipm_stage + polish_rounds * pol_stage)
+
+
+def dense_flop(H: int, n_stance: float, ipm_iters: float, polish_rounds: float) -> float:
+    """Useful flops of one QP on the condensed dense interior point (lmpc_dense.hip): SURVEY.md 8(d)'s formulas with
+    the condensed dimension the kernel solves, N = 3 x stance leg-steps (swing leg-steps are eliminated exactly), and
+    the condensation's Hessian columns priced per stance variable: free response + adjoint 2 x 12 x 12 H, cost-to-go
+    c H, H columns N x (12 x 6 + H x 8 + stance variables of the later steps x 6) ~ N (72 + 8 H) + N^2 x 6 / 2;
+    per interior-point iteration M = H + C'WC, its Cholesky N^3 / 3, two Newton systems of two triangular solves
+    (4 x 2 N^2 / 2); per polish round T'HT (2 N^2 x 3 / 3), the Cholesky, one system and H u (2 N^2)."""
+    N = 3.0 * n_stance
+    c = 2 * 12 ** 3
+    cond = 2 * 2 * 144 * H + c * H + 2 * N * (72 + 8 * H) + 6 * N * N
+    it = N * N / 2 + N ** 3 / 3 + 4 * N * N
+    pol = 2 * N * N + N ** 3 / 3 + 2 * N * N + 2 * N * N
+    return cond + ipm_iters * it + polish_rounds * pol
+
+
 def survey_f0(H: int) -> float:
     N = 12 * H
     c = 2 * 12 ** 3

@@ -214,7 +214,7 @@ class BatchedConvexQPSolver:
 
     def synth_commands_device(self, cfg: N.LmpcSynthCfg, count: int, seed: int, first_index: int = 0, device=None,
                               stream=None):
-        """Synthetic commands generated on the device from (seed, global index) -> uint8 [count, 384]."""
+        """Synthetic commands generated on the device from (seed, global index) -> uint8 [count, 408]."""
         import torch
 
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
@@ -236,7 +236,7 @@ class BatchedConvexQPSolver:
         return out
 
     def build_records_device(self, cmd, stream=None):
-        """uint8 [B, 384] commands in HBM -> (rec [B, 33+12H] f64, contact [B, H, 4] u8) in HBM."""
+        """uint8 [B, 408] commands in HBM -> (rec [B, 33+12H] f64, contact [B, H, 4] u8) in HBM."""
         import torch
 
         B = cmd.shape[0]

@@ -62,3 +62,25 @@ def lmpc_params_from(pr):
 
 def rel_err(a, b):
     return float(np.max(np.abs(np.asarray(a) - np.asarray(b)) / np.maximum(1.0, np.abs(np.asarray(b)))))
+
+
+def fsm_commands(count, seed, H=10):
+    """Synthetic commands (config-4 states) whose four legs carry the phases and FSM states of the reference's leg
+    FSMs after a random walk of MPC ticks with early touchdowns (oracle/fsm.py): the per-leg phases differ and some are
+    negative (LeggedContactFSM.cpp:61-66,214-221).  -> (ctypes LmpcCommand array, list of the four FSMs per command)."""
+    from legged_mpc_control_amd import synth
+    from oracle import fsm as F
+
+    rng = np.random.default_rng(seed)
+    cmds = synth.commands(synth.config_cfg(4), count, synth.BASE_SEED + 4, first_index=500 + seed)
+    fsms = []
+    for b in range(count):
+        gait = int(rng.integers(0, 3))  # trot, crawl, trot with stand (a stand never swings)
+        fs = F.random_walk(rng, gait, 4.0, ticks=int(rng.integers(1, 200)))
+        c = cmds[b]
+        c.gait, c.gait_speed = gait, 4.0
+        for j in range(4):
+            c.gait_phase[j] = fs[j].phase
+            c.plan_contacts[j] = fs[j].s
+        fsms.append(fs)
+    return cmds, fsms

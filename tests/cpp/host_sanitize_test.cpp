@@ -65,8 +65,8 @@ static void host_helpers(const lmpc_params& p) {
             CHECK(lmpc_command_to_record(&p, H, &cmd[b], rec2.data() + (size_t)b * RL, con2.data() + (size_t)b * 4 * H) ==
                       LMPC_OK, "cmd->rec");
             std::vector<uint8_t> sched(4 * H);
-            lmpc_contact_schedule(cmd[b].gait, cmd[b].gait_phase, cmd[b].gait_speed, p.dt, H, cmd[b].plan_contacts,
-                                  sched.data());
+            lmpc_contact_schedule_legs(cmd[b].gait, cmd[b].gait_phase, cmd[b].gait_speed, p.dt, H, cmd[b].plan_contacts,
+                                       sched.data());
             CHECK(std::memcmp(sched.data(), con.data() + (size_t)b * 4 * H, 4 * H) == 0, "schedule H=%d b=%d", H, b);
             double vdw[3];
             std::vector<double> r3(RL);

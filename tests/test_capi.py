@@ -38,7 +38,7 @@ def test_exports_are_c_linkage():
 
 def test_abi_and_strings():
     lib = N.lib()
-    assert lib.lmpc_abi_version() == 6
+    assert lib.lmpc_abi_version() == 7
     assert lib.lmpc_record_len(10) == 153 and lib.lmpc_record_len(30) == 393
     assert lib.lmpc_strerror(0) == b"ok"
     assert lib.lmpc_strerror(-1) == b"invalid argument"
@@ -46,10 +46,12 @@ def test_abi_and_strings():
 
 def test_struct_layouts():
     assert ctypes.sizeof(N.LmpcParams) == 8 * (12 + 12 + 1 + 9 + 4)
-    assert ctypes.sizeof(N.LmpcOptions) == 4 * 3 + 4 + 8 * 3 + 4 * 4  # 3 ints + pad + 3 doubles + 4 ints (ABI 5)
+    # 3 ints + pad + 3 doubles + 4 ints (ABI 5) + tol_x (ABI 7)
+    assert ctypes.sizeof(N.LmpcOptions) == 4 * 3 + 4 + 8 * 3 + 4 * 4 + 8
     assert ctypes.sizeof(N.LmpcStateIn) == 8 * (3 * 4 + 9 + 12 + 3 * 4)
-    assert ctypes.sizeof(N.LmpcCommand) == N.COMMAND_BYTES == 384  # static_assert'ed in lmpc_common.h
-    assert N.LmpcCommand.gait.offset == 376 and N.LmpcCommand.plan_contacts.offset == 380
+    assert ctypes.sizeof(N.LmpcCommand) == N.COMMAND_BYTES == 408  # static_assert'ed in lmpc_common.h
+    assert N.LmpcCommand.gait_phase.offset == 360 and N.LmpcCommand.gait.offset == 400
+    assert N.LmpcCommand.plan_contacts.offset == 404
 
 
 def test_create_rejects_bad_arguments():

@@ -364,6 +364,8 @@ def test_failed_crossover_below_an_exact_level_meets_the_true_bounds(hq, tol_mu)
                         assert viol <= 1e-7 * scale, f"{group}[{b}] level {l}: level {j} row violated by {viol:.2e}"
                     o += s
     print(f"tol_mu {tol_mu:g}: {hit} levels below an exact level kept a failed crossover's iterate")
+    if tol_mu == 1e-4:  # the path under test must be reached (8 such levels on the golden groups, round 4)
+        assert hit > 0, "no level below an exact level kept a failed crossover's iterate: the true-bound path is untested"
 
 
 def test_crossover_off_keeps_the_interior_point_iterate(hq):

@@ -79,6 +79,26 @@ def test_lq_two_wave_instance_vs_oracle(cid):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H,terrain", [(4, False), (7, True), (11, False), (11, True), (16, False), (16, True)])
+def test_lq_two_wave_instance_other_horizons(H, terrain):
+    """the two-waves-per-SIMD instance (batches above one QP per SIMD) at H != 10 -- H < 10 and H = 11..16,
+    where the closed-loop rows are not kept (H > 10) -- with and without terrain: every QP of a 2048-QP batch against
+    the oracle, and the batch's bits equal to the lone-wave instance's on 512 of the same records (a QP's answer must
+    not depend on the batch it is solved in)."""
+    from legged_mpc_control_amd import synth
+
+    count = 2048
+    p, _, rec, con = synth.config_batch(4, count=count, first_index=100 * H, H=H)
+    nrm = synth.config_normals(4, count, 100 * H) if terrain else None
+    g, st, _ = _solver(p, H, count).solve(rec, con, normals=nrm)
+    assert (st == 0).all(), np.unique(st, return_counts=True)
+    assert _err(g, _oracle(p, H, rec, con, nrm)) <= TOL
+    sl = slice(256, 768)
+    g1, st1, _ = _solver(p, H, 512).solve(rec[sl], con[sl], normals=None if nrm is None else nrm[sl])
+    assert np.array_equal(st1, st[sl]) and np.array_equal(g1, g[sl])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H", [1, 2, 10, 16, 17, 32])
 def test_lq_horizon_range(H):
     """LS = 1 (H <= 16, two waves per SIMD) and LS = 2 (H > 16) instances, the whole horizon range."""

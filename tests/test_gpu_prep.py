@@ -6,7 +6,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import rel_err
+from conftest import fsm_commands, rel_err
 
 from legged_mpc_control_amd import BatchedConvexQPSolver, _native as N, synth
 from oracle import oracle as O
@@ -43,6 +43,33 @@ def test_device_expansion_bit_identical(cid, dev):
     assert np.array_equal(d_con.cpu().numpy(), con)
 
 
+def test_device_expansion_per_leg_phases(dev):
+    """ABI 7: commands whose legs carry diverged FSM phases (early touchdowns, negative phases; oracle/fsm.py) expand
+    on the device to the host's records and schedules bit for bit, every leg predicted from its own phase; the
+    solve of those QPs matches the oracle."""
+    import torch
+
+    from oracle import fsm as F
+
+    p, H = synth.params("go1"), 10
+    cmds, fsms = fsm_commands(1024, seed=9, H=H)
+    s = BatchedConvexQPSolver(p, H, max_batch=0)
+    d_rec, d_con = s.build_records_device(_host_cmds_tensor(cmds, dev))
+    torch.cuda.synchronize()
+    con = d_con.cpu().numpy()
+    for b in range(len(cmds)):
+        r, c = synth.command_to_record(p, H, cmds[b])
+        assert np.array_equal(c, con[b]) and np.array_equal(c, np.array(F.schedule(fsms[b], H, p.dt), dtype=np.uint8))
+        assert np.array_equal(r, d_rec[b].cpu().numpy())
+    grf = torch.empty((len(cmds), H, 12), dtype=torch.float64, device=dev)
+    st = torch.empty(len(cmds), dtype=torch.int32, device=dev)
+    s.solve_commands_device(_host_cmds_tensor(cmds, dev), grf, st)
+    torch.cuda.synchronize()
+    ref, _, fails = O.solve_batch(O.params_from(p), H, d_rec.cpu().numpy(), con, n_threads=8)
+    assert fails == 0 and np.all(st.cpu().numpy() == 0)
+    assert rel_err(grf.cpu().numpy(), ref) <= 1e-7
+
+
 def test_device_generator_matches_host(dev):
     import torch
 
@@ -54,10 +81,11 @@ def test_device_generator_matches_host(dev):
     host = synth.commands(cfg, 4096, 123, first_index=1000)
     hraw = np.frombuffer(bytes(host), dtype=np.uint8).reshape(4096, N.COMMAND_BYTES)
     draw = d_cmd.cpu().numpy()
-    hd, dd = hraw[:, :376].view(np.float64), draw[:, :376].view(np.float64)  # 45 state doubles + phase + speed
+    # 45 state doubles + 4 per-leg phases + speed
+    hd, dd = hraw[:, :400].view(np.float64), draw[:, :400].view(np.float64)
     assert np.max(np.abs(hd - dd) / np.maximum(1.0, np.abs(hd))) <= 1e-14
-    assert np.array_equal(hraw[:, 376:], draw[:, 376:])  # gait, plan_contacts (and padding-free tail)
-    assert np.array_equal(hd[:, 45], dd[:, 45])  # gait phase: no transcendental on its path
+    assert np.array_equal(hraw[:, 400:], draw[:, 400:])  # gait, plan_contacts (and padding-free tail)
+    assert np.array_equal(hd[:, 45:49], dd[:, 45:49])  # gait phases: no transcendental on their path
     # normals
     dn = s.synth_normals_device(4096, 123, first_index=1000, device=dev)
     torch.cuda.synchronize()

@@ -6,7 +6,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import golden_files, load_golden
+from conftest import fsm_commands, golden_files, load_golden
 
 from legged_mpc_control_amd import _native as N
 from legged_mpc_control_amd import synth
@@ -67,6 +67,45 @@ def test_contact_schedule_matches_fsm():
             for i in range(1, 12):
                 for j in range(4):
                     assert out[i, j] == O.predict_contact(gait, j, phase, 4.0, 0.01 * i)
+
+
+def test_per_leg_phases_follow_each_leg_fsm():
+    """ABI 7: lmpc_command carries one phase per leg, and the expansion predicts every leg from
+    its own phase (ConvexQPSolver.cpp:341-342), bit for bit against an independent restatement of the reference's
+    four leg FSMs after early touchdowns (oracle/fsm.py: negative phases included)."""
+    from oracle import fsm as F
+
+    H = 10
+    p = synth.params("go1")
+    cmds, fsms = fsm_commands(400, seed=5, H=H)
+    phases = np.array([[c.gait_phase[j] for j in range(4)] for c in cmds])
+    assert (phases < 0).any() and (np.ptp(phases, axis=1) > 0.02).any()  # wrapped and diverged legs
+    rec_ref, _ = synth.fill(p, synth.config_cfg(4), H, 400, synth.BASE_SEED + 4, first_index=505)
+    L = N.lib()
+    u8 = ctypes.POINTER(ctypes.c_uint8)
+    for b in range(400):
+        want = np.array(F.schedule(fsms[b], H, p.dt), dtype=np.uint8)
+        r, c = synth.command_to_record(p, H, cmds[b])
+        assert np.array_equal(c, want), b
+        assert np.array_equal(r, rec_ref[b])  # the record does not depend on the gait state
+        out = np.zeros((H, 4), dtype=np.uint8)
+        ph = np.array(phases[b])
+        plan = np.array([cmds[b].plan_contacts[j] for j in range(4)], dtype=np.uint8)
+        N.check(L.lmpc_contact_schedule_legs(cmds[b].gait, ph.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 4.0,
+                                             p.dt, H, plan.ctypes.data_as(u8), out.ctypes.data_as(u8)))
+        assert np.array_equal(out, want), b
+        for i in range(1, H):
+            for j in range(4):
+                assert want[i, j] == L.lmpc_predict_contact(cmds[b].gait, j, phases[b, j], 4.0, p.dt * i)
+    # equal phases reduce to the single-phase schedule (the pre-ABI-7 command)
+    for gait in range(4):
+        one, legs = np.zeros((H, 4), dtype=np.uint8), np.zeros((H, 4), dtype=np.uint8)
+        plan = np.ones(4, dtype=np.uint8)
+        ph = np.full(4, 0.37)
+        N.check(L.lmpc_contact_schedule(gait, 0.37, 4.0, p.dt, H, plan.ctypes.data_as(u8), one.ctypes.data_as(u8)))
+        N.check(L.lmpc_contact_schedule_legs(gait, ph.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 4.0, p.dt, H,
+                                             plan.ctypes.data_as(u8), legs.ctypes.data_as(u8)))
+        assert np.array_equal(one, legs)
 
 
 def test_current_contact_is_fsm_state():
