@@ -11,42 +11,14 @@ flops of one QP of horizon H, independent of how the build solves it --
 with K the measured mean interior-point iterations and `rounds` the mean polish rounds.
 F0 = 1.544M / 10.72M / 34.44M flop at H = 10 / 20 / 30.
 
-`qp_flop` is the build's own count of useful fp64 flops of its Riccati formulation (FMA = 2
-flops), per horizon stage, reported beside it:
-
-  Riccati factorisation stage (riccati_factor):
-    Bt = G0 T (216 FMA) + G0 up (72) + PB = P[:,6:12] Bt (864) + v = P d (72)
-    + Guu = T'RtT + Bt'PB[6:12] (324 + 864) + Gux = PB'A (180)
-    + Cholesky(12) + L^-1 Gux + L^-1 (288 + 864 + 288)
-    + P(I+dtN), (I+dtN')PA (500) + Y'Y symmetric (936)            = 5468 FMA
-  Riccati vector pass stage (riccati_solve): backward 450 FMA + forward 410 = 860 FMA
-  Adjoint stage (adjoint_grad): 120 FMA
-  IPM iteration  = 1 factorisation + 2 vector passes (predictor + corrector)
-  polish round   = 1 factorisation + 1 vector pass + 1 adjoint
+`lq_flop` (the LDS Riccati kernel) and `dense_flop` (the condensed dense interior point) are the useful flops of
+the formulations the kernels run, reported beside it and used as the headline fraction wherever the contract's F0 (a
+dense N = 12H condensation) is not the work done.
 """
 from __future__ import annotations
 
-FACT_FLOP_PER_STAGE = 2 * 5468
-SOLVE_FLOP_PER_STAGE = 2 * 860
-ADJ_FLOP_PER_STAGE = 2 * 120
-LEG_FLOP_PER_IPM_ITER = 2 * 60      # per stance leg-step: W, C'WC, C'w, step lengths
-LEG_FLOP_PER_POLISH = 2 * 80        # per stance leg-step: null basis + verification
-
 FP64_PEAK_TFLOPS = 78.6             # MI355X FP64 (vector = matrix), SURVEY.md 8d / AMD spec
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
-
-
-def ipm_iter_flop(H: int) -> int:
-    return H * (FACT_FLOP_PER_STAGE + 2 * SOLVE_FLOP_PER_STAGE) + 4 * H * LEG_FLOP_PER_IPM_ITER
-
-
-def polish_round_flop(H: int) -> int:
-    return H * (FACT_FLOP_PER_STAGE + SOLVE_FLOP_PER_STAGE + ADJ_FLOP_PER_STAGE) + 4 * H * LEG_FLOP_PER_POLISH
-
-
-def qp_flop(H: int, ipm_iters: float, polish_rounds: float) -> float:
-    """Algorithmic flops of one QP given its (mean) IPM iterations and polish rounds."""
-    return ipm_iters * ipm_iter_flop(H) + polish_rounds * polish_round_flop(H)
 
 
 # ---- the LDS Riccati kernel (lmpc_lq.hip, round 4 on): useful flops of the formulation it runs -----------------
