@@ -57,6 +57,8 @@ public:
         act_in_.assign((size_t)4 * H_, 0);
         error_ = lmpc_create(&params_, H_, 1, device_, &ctx_);
         if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_IPM);
+        // warm start is on by default: its workspace now, not at the first tick
+        if (error_ == LMPC_OK) error_ = lmpc_reserve_warm(ctx_, 1);
     }
     ~ConvexQPSolver() { lmpc_destroy(ctx_); }
     ConvexQPSolver(const ConvexQPSolver&) = delete;

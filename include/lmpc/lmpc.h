@@ -167,6 +167,10 @@ int lmpc_get_riccati_path(const lmpc_ctx* ctx);
  * path's hand-over flags and, with LMPC_RICCATI_SCRATCH, the factor workspace (the device path grows them on
  * demand; call this after lmpc_set_riccati_path and before capturing a HIP graph). */
 int lmpc_reserve(lmpc_ctx* ctx, int batch);
+/* ABI 7: also the warm-start workspace (warm-started solves, lmpc_solve_batch_warm, always run on the scratch kernel):
+ * a host that warm-starts calls this once at set-up, so the first warm solve does not allocate (hipMalloc and a
+ * device-wide synchronisation) inside the control loop.  The drop-in classes do it in their constructors. */
+int lmpc_reserve_warm(lmpc_ctx* ctx, int batch);
 
 /* Host buffers in/out, synchronous.  rec[batch][33+12H], contact[batch][H][4],
  * grf[batch][H][12]; status[batch] and iters[batch] may be NULL. */

@@ -35,8 +35,8 @@ EXPORTED_SYMBOLS = (
     "lmpc_leg_kin_default", "lmpc_foot_jacobian", "lmpc_grf_to_torque", "lmpc_grf_to_torque_device",
     # ABI 3: dense-path selection
     "lmpc_set_dense_path", "lmpc_get_dense_path", "lmpc_set_riccati_path", "lmpc_get_riccati_path",
-    # ABI 7: per-leg gait phases
-    "lmpc_contact_schedule_legs",
+    # ABI 7: per-leg gait phases, warm-start workspace
+    "lmpc_contact_schedule_legs", "lmpc_reserve_warm",
 )
 ABI_VERSION = 7
 # include/lmpc/lmpc_hoqp.h: batched hierarchical QP (whole-body control)
@@ -204,6 +204,9 @@ def lib():
         L.lmpc_get_riccati_path.restype = ctypes.c_int
         L.lmpc_reserve.argtypes = [vp, ctypes.c_int]
         L.lmpc_reserve.restype = ctypes.c_int
+        if hasattr(L, "lmpc_reserve_warm"):  # ABI 7
+            L.lmpc_reserve_warm.argtypes = [vp, ctypes.c_int]
+            L.lmpc_reserve_warm.restype = ctypes.c_int
         L.lmpc_solve_batch.argtypes = [vp, dp, u8p, ctypes.c_int, dp, i32p, i32p]
         L.lmpc_solve_batch.restype = ctypes.c_int
         L.lmpc_solve_batch_device.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]

@@ -30,6 +30,8 @@ ConvexQPSolver::ConvexQPSolver(const double* q_weights, const double* r_weights,
     // active set, tools/single_qp_latency.py).  The Python drop-in (legged_mpc_control_amd.ConvexQPSolver) has
     // the same defaults.
     if (error_ == LMPC_OK) error_ = lmpc_set_dense_path(ctx_, LMPC_DENSE_IPM);
+    // the warm-start workspace now, not inside the first tick (hipMalloc + a device-wide synchronisation)
+    if (error_ == LMPC_OK) error_ = lmpc_reserve_warm(ctx_, 1);
 }
 
 ConvexQPSolver::~ConvexQPSolver() { lmpc_destroy(ctx_); }

@@ -323,6 +323,11 @@ int lmpc_reserve(lmpc_ctx* c, int batch) {
     return ensure_ws(c, batch, c->riccati == LMPC_RICCATI_SCRATCH);
 }
 
+int lmpc_reserve_warm(lmpc_ctx* c, int batch) {
+    if (!c || batch < 0) return LMPC_ERR_ARG;
+    return ensure_ws(c, batch, true);
+}
+
 int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* d_contact, const double* d_normals,
                                int batch, double* d_grf, int32_t* d_status, int32_t* d_iters, void* stream) {
     if (!c || batch < 0 || (batch > 0 && (!d_rec || !d_contact || !d_grf))) return LMPC_ERR_ARG;

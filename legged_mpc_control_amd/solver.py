@@ -86,6 +86,14 @@ class BatchedConvexQPSolver:
             self.set_dense_path(dense_path)
         if riccati_path is not None:
             self.set_riccati_path(riccati_path)
+        if self.max_batch > 0:
+            # the workspace of the context's paths for max_batch QPs (after the Riccati path is chosen: the scratch
+            # kernel's factors are reserved only when it runs)
+            N.check(self._L.lmpc_reserve(self._ctx, self.max_batch), "lmpc_reserve")
+
+    def reserve_warm(self, batch: int) -> None:
+        """Pre-allocate the warm-start workspace (lmpc_reserve_warm) so the first warm solve does not allocate."""
+        N.check(self._L.lmpc_reserve_warm(self._ctx, int(batch)), "lmpc_reserve_warm")
 
     def set_riccati_path(self, path: str) -> None:
         N.check(self._L.lmpc_set_riccati_path(self._ctx, self.RICCATI_PATHS[path]), "lmpc_set_riccati_path")
@@ -391,6 +399,7 @@ class ConvexQPSolver:
         # warm-starts too, ConvexQPSolver.cpp:185); cold solves (set_warm_start(False)) take the condensed
         # interior point, since round 3 also the lower-latency dense kernel for one QP per call.
         self._dev = BatchedConvexQPSolver(p, self.H, 1, device, dense_path="ipm")
+        self._dev.reserve_warm(1)
         self._rec = np.zeros((1, 33 + 12 * self.H))
         self._con = np.ones((1, self.H, 4), dtype=np.uint8)
         self._warm = True
