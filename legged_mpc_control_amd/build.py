@@ -21,17 +21,26 @@ HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 # 0.2198-0.2212 ms, config 4 19.61 -> 19.07-19.18 ms; iterative-ilp: the dual active set (config 2 --dense gi)
 # 0.469 -> 0.459-0.461 ms, the WBC hierarchies 4.89 -> 4.78 ms.  (iterative-ilp crashes the compiler on
 # lmpc_prep.hip, which keeps the default.)
+# The dense path and the LDS Riccati kernel contract a * b + c into an fma only within one source expression
+# (-ffp-contract=on; HIP's default contracts across statements in the backend, where the result depends on how
+# the surrounding code happens to split into basic blocks): a QP's bits must not depend on the kernel instance
+# or launch that solves it (one- or two-wave Riccati instance, the fused dense + Riccati launch -- round 5 found
+# the default broke that identity once the kernel bodies became shared device functions), and the dense body is
+# compiled into both lmpc_dense.hip and lmpc_lq.hip.  Measured (tools/ab_bench.sh, two alternating runs): configs
+# 2-5 0.6-1.4 % faster than HEAD, every GPU test at its old tolerance.
+FP_CONTRACT = ["-ffp-contract=on"]
 SCHED_FLAGS = {
     "lmpc_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-    "lmpc_dense.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-    "lmpc_lq.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "lmpc_dense.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + FP_CONTRACT,
+    "lmpc_lq.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + FP_CONTRACT,
     "lmpc_gi.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
     "lmpc_hoqp.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
 
 SOURCES = ["lmpc_kernels.hip", "lmpc_lq.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
            "hoqp_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
-HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_hoqp_device.h"]
+HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_dense_kernel.h",
+           "lmpc_hoqp_device.h"]
 
 
 def hipcc() -> str:

@@ -24,6 +24,8 @@ hipError_t launch_gi(const DevParams& prm, const double* rec, const uint8_t* con
                      int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
 hipError_t launch_dense(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
                         int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
+hipError_t launch_dense_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                           int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream);
 hipError_t launch_records(const lmpc_command* cmd, int batch, int H, double dt, double* rec, uint8_t* contact,
                           hipStream_t stream);
 hipError_t launch_synth(const lmpc_synth_cfg& cfg, uint64_t seed, int64_t first, int count, lmpc_command* cmd,
@@ -342,14 +344,25 @@ int lmpc_solve_batch_device_ex(lmpc_ctx* c, const double* d_rec, const uint8_t* 
     }
     hipError_t e = ctx_enter(c, s);
     // condensed dense kernel first; it flags the QPs it solved and the Riccati kernel solves the rest
-    // (more than 20 stance leg-steps, or a dense QP left without a verified optimum)
-    if (e == hipSuccess && c->prm.dense == 2)
-        e = lmpc::launch_gi(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
-    else if (e == hipSuccess && c->prm.dense == 1)
-        e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
-    if (e == hipSuccess)
-        e = launch_riccati(c, c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters,
-                           c->prm.dense ? c->d_done : nullptr, s);
+    // (more than 20 stance leg-steps, or a dense QP left without a verified optimum).  At most one QP per SIMD
+    // (both kernels one wave per SIMD) the two run as one launch, each QP's Riccati solve after its dense one in
+    // the same wave (lmpc_dense_lq_kernel, the same arithmetic)
+    bool fused = false;
+    if (e == hipSuccess && c->prm.dense == 1 && !uses_scratch(c, c->prm)) {
+        const hipError_t f = lmpc::launch_dense_lq(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status,
+                                                    d_iters, c->d_done, s);
+        if (f == hipSuccess) fused = true;
+        else if (f != hipErrorNotSupported) e = f;
+    }
+    if (!fused) {
+        if (e == hipSuccess && c->prm.dense == 2)
+            e = lmpc::launch_gi(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
+        else if (e == hipSuccess && c->prm.dense == 1)
+            e = lmpc::launch_dense(c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters, c->d_done, s);
+        if (e == hipSuccess)
+            e = launch_riccati(c, c->prm, d_rec, d_contact, d_normals, batch, d_grf, d_status, d_iters,
+                               c->prm.dense ? c->d_done : nullptr, s);
+    }
     if (e == hipSuccess) e = ctx_leave(c, s);
     if (e == hipErrorInvalidDeviceFunction || e == hipErrorNoBinaryForGpu) return LMPC_ERR_NOT_BUILT;
     return e == hipSuccess ? LMPC_OK : LMPC_ERR_LAUNCH;

@@ -39,9 +39,22 @@
 #include <cstdint>
 #include <type_traits>
 
+#include <algorithm>
+
 #include "lmpc/lmpc.h"
 #include "lmpc_device.h"
 #include "lmpc_kernel_common.h"
+
+// The fused dense + Riccati kernel (lmpc_dense_lq_kernel, below) in the product build; the diagnostic and test-variant
+// builds (stamps, certificate residuals, re-injected bugs, debug dumps) keep the two launches, so their hooks live in
+// one translation unit each
+#if !defined(LMPC_STAMPS) && !defined(LMPC_KKT_DIAG) && !defined(LMPC_BUG_ZA) && !defined(LMPC_BUG_YAW) && \
+    !defined(LMPC_KKT_OFF) && !defined(LMPC_LQ_DEBUG) && !defined(LMPC_NO_FUSED)
+#define LMPC_FUSED 1
+#include "lmpc_dense_kernel.h"
+#else
+#define LMPC_FUSED 0
+#endif
 
 namespace lmpc {
 
@@ -219,19 +232,20 @@ __device__ __forceinline__ void sym3_solve(const double R[6], const double b[3],
 // WPE = waves per SIMD the register budget allows: 2 (256 registers, LS = 1 only: eight QPs per CU at H <= 10) or 1
 // (512, no spills: the instance for batches of at most one QP per SIMD, and for LS = 2).
 // ---------------------------------------------------------------------------------------------------------
+// The solve of QP blockIdx.x as a device function: lmpc_lq_kernel runs it alone; lmpc_dense_lq_kernel after the dense
+// solve of the same QP (after_dense: the QP is one the dense solve left, so the hand-over test below is skipped).
 template <int LS, bool TERRAIN, int WPE>
-__global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, const double* __restrict__ rec,
-                                                                     const uint8_t* __restrict__ contact,
-                                                                     const double* __restrict__ normals, int batch,
-                                                                     double* __restrict__ grf, int32_t* __restrict__ status,
-                                                                     int32_t* __restrict__ iters,
-                                                                     const uint8_t* __restrict__ dense_done) {
+__device__ __forceinline__ void lq_body(const DevParams prm, const double* __restrict__ rec,
+                                        const uint8_t* __restrict__ contact, const double* __restrict__ normals,
+                                        int batch, double* __restrict__ grf, int32_t* __restrict__ status,
+                                        int32_t* __restrict__ iters, const uint8_t* __restrict__ dense_done,
+                                        bool after_dense) {
     extern __shared__ __attribute__((aligned(16))) double lq_smem[];
     const int qp = blockIdx.x;
     if (qp >= batch) return;
     const int lane = threadIdx.x;
     const int H = prm.H;
-    if (prm.dense) {  // QPs with 1..DENSE_MAX_LS stance leg-steps went to a dense-path kernel (H <= 16 here)
+    if (prm.dense && !after_dense) {  // QPs with 1..DENSE_MAX_LS stance leg-steps went to a dense-path kernel (H <= 16 here)
         const bool stl = lane < 4 * H && contact[(size_t)qp * 4 * H + lane] != 0;
         const int n = __popcll(__ballot(stl));
         if (n >= 1 && n <= DENSE_MAX_LS && (!dense_done || dense_done[qp])) return;
@@ -1619,6 +1633,37 @@ __global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, c
     LQ_STAMP_FLUSH(qp);
 }
 
+template <int LS, bool TERRAIN, int WPE>
+__global__ void __launch_bounds__(64, WPE) lmpc_lq_kernel(const DevParams prm, const double* __restrict__ rec,
+                                                          const uint8_t* __restrict__ contact,
+                                                          const double* __restrict__ normals, int batch,
+                                                          double* __restrict__ grf, int32_t* __restrict__ status,
+                                                          int32_t* __restrict__ iters,
+                                                          const uint8_t* __restrict__ dense_done) {
+    lq_body<LS, TERRAIN, WPE>(prm, rec, contact, normals, batch, grf, status, iters, dense_done, false);
+}
+
+#if LMPC_FUSED
+// The dense path and the Riccati kernel in one launch, for batches of at most one QP per SIMD (config 2: B = 1024
+// on 256 CUs), where both run one wave per SIMD anyway: the dense solve of each QP, then -- in the same wave, for
+// the QPs it leaves -- the lone-wave Riccati solve.  The same two solves as the two launches (bit for bit), without
+// the second launch and its dispatch of a workgroup per QP that only tests the hand-over flag (~4 us + the gap
+// between the launches, ~5 % of config 2's step).
+template <bool TERRAIN>
+__global__ void __launch_bounds__(64, 1) lmpc_dense_lq_kernel(const DevParams prm, const double* __restrict__ rec,
+                                                              const uint8_t* __restrict__ contact,
+                                                              const double* __restrict__ normals, int batch,
+                                                              double* __restrict__ grf, int32_t* __restrict__ status,
+                                                              int32_t* __restrict__ iters, uint8_t* __restrict__ done) {
+    if (!dense_body<TERRAIN>(prm, rec, contact, normals, batch, grf, status, iters, done))
+        lq_body<1, TERRAIN, 1>(prm, rec, contact, normals, batch, grf, status, iters, done, true);
+}
+template __global__ void lmpc_dense_lq_kernel<false>(const DevParams, const double*, const uint8_t*, const double*,
+                                                     int, double*, int32_t*, int32_t*, uint8_t*);
+template __global__ void lmpc_dense_lq_kernel<true>(const DevParams, const double*, const uint8_t*, const double*,
+                                                    int, double*, int32_t*, int32_t*, uint8_t*);
+#endif
+
 #define LMPC_LQ_INST(LS_, T_, W_)                                                                                    \
     template __global__ void lmpc_lq_kernel<LS_, T_, W_>(const DevParams, const double*, const uint8_t*, const double*, \
                                                      int, double*, int32_t*, int32_t*, const uint8_t*);
@@ -1672,6 +1717,34 @@ hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* con
     }
 #undef LMPC_LQ_LAUNCH
     return hipGetLastError();
+}
+
+// One launch for the dense path (interior point) and the Riccati solves it leaves, where both would run one wave per
+// SIMD (batch <= 4 x CUs, H <= 16): lmpc_dense_lq_kernel.  hipErrorNotSupported where this build has no fused kernel
+// (diagnostic builds) or the batch does not qualify: the caller then launches the two kernels.
+hipError_t launch_dense_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals,
+                           int batch, double* grf, int32_t* status, int32_t* iters, uint8_t* done, hipStream_t stream) {
+#if LMPC_FUSED
+    if (4 * prm.H > 64 || batch > 4 * prm.cus) return hipErrorNotSupported;
+    const size_t lds = std::max(dense_lds_bytes(prm.H), lq_lds_bytes(prm.H));
+    const dim3 grid(batch), block(LMPC_WAVE);
+    if (normals) {
+        (void)hipFuncSetAttribute((const void*)lmpc_dense_lq_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL(lmpc_dense_lq_kernel<true>, grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
+                           status, iters, done);
+    } else {
+        (void)hipFuncSetAttribute((const void*)lmpc_dense_lq_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL(lmpc_dense_lq_kernel<false>, grid, block, lds, stream, prm, rec, contact, normals, batch, grf,
+                           status, iters, done);
+    }
+    return hipGetLastError();
+#else
+    (void)prm, (void)rec, (void)contact, (void)normals, (void)batch, (void)grf, (void)status, (void)iters, (void)done;
+    (void)stream;
+    return hipErrorNotSupported;
+#endif
 }
 
 #ifdef LMPC_STAMPS
