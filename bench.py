@@ -69,11 +69,14 @@ def host_cores():
     return usable, {"os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota}
 
 
-def kernel_label(mode, riccati="lds"):
+def kernel_label(mode, riccati="lds", fused=False):
     """The kernels of one solve launch (lmpc_capi.cpp lmpc_solve_batch_device_ex); kernel_ms covers all."""
     ric = "lmpc_lq_kernel" if riccati == "lds" else "lmpc_qp_kernel"
     if mode == "off":
         return f"{ric} (Riccati, every QP)"
+    if fused:
+        return ("lmpc_dense_lq_kernel (one launch: the dense interior point for QPs with <= 20 stance leg-steps, "
+                "the lone-wave Riccati solve in the same wave for the rest)")
     dense = "lmpc_gi_kernel" if mode == "gi" else "lmpc_dense_kernel"
     return f"{dense} (QPs with <= 20 stance leg-steps) + {ric} (the rest; exits at once when none)"
 
@@ -391,7 +394,8 @@ def main():
                 **({"contract_flop_per_qp": contract_per_qp,
                     "contract_model": flop_model} if headline_contract else {}),
                 "traffic": traffic_bytes,
-                "kernel": kernel_label(mode, args.riccati),
+                "kernel": kernel_label(mode, args.riccati, fused=mode == "ipm" and args.riccati == "lds" and 4 * H <= 64
+                                       and B <= 4 * torch.cuda.get_device_properties(dev).multi_processor_count),
                 "kernel_ms": kernel_ms,
                 "executed": executed,
                 "hbm_gbs": roofline.qp_bytes(H) * B / (kernel_ms * 1e-3) / 1e9,

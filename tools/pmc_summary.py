@@ -28,7 +28,8 @@ def rows(name):
     return list(csv.DictReader(open(os.path.join(SRC, name, f"{name}_counter_collection.csv"))))
 
 
-SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_gi_kernel", "lmpc_qp_kernel", "lmpc_lq_kernel")  # one solve launch = a dense-path kernel + the Riccati kernel
+# one solve launch = a dense-path kernel + the Riccati kernel, or the fused dense + Riccati kernel (round 5)
+SOLVE_KERNELS = ("lmpc_dense_kernel", "lmpc_gi_kernel", "lmpc_qp_kernel", "lmpc_lq_kernel", "lmpc_dense_lq_kernel")
 
 
 def per_kernel(name, kern, counter=None):
