@@ -21,25 +21,33 @@ HIP_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 # 0.2198-0.2212 ms, config 4 19.61 -> 19.07-19.18 ms; iterative-ilp: the dual active set (config 2 --dense gi)
 # 0.469 -> 0.459-0.461 ms, the WBC hierarchies 4.89 -> 4.78 ms.  (iterative-ilp crashes the compiler on
 # lmpc_prep.hip, which keeps the default.)
-# The dense path and the LDS Riccati kernel contract a * b + c into an fma only within one source expression
-# (-ffp-contract=on; HIP's default contracts across statements in the backend, where the result depends on how
-# the surrounding code happens to split into basic blocks): a QP's bits must not depend on the kernel instance
-# or launch that solves it (one- or two-wave Riccati instance, the fused dense + Riccati launch -- round 5 found
-# the default broke that identity once the kernel bodies became shared device functions), and the dense body is
-# compiled into both lmpc_dense.hip and lmpc_lq.hip.  Measured (tools/ab_bench.sh, two alternating runs): configs
-# 2-5 0.6-1.4 % faster than HEAD, every GPU test at its old tolerance.
-FP_CONTRACT = ["-ffp-contract=on"]
+# Floating-point contract of the dense path and the LDS Riccati kernel (the dense body is compiled into both
+# lmpc_dense.hip and lmpc_lq.hip):
+#   -ffp-contract=on: a * b + c becomes an fma only within one source expression (HIP's default contracts across
+#     statements in the backend, where the result depends on how the surrounding code happens to split into basic
+#     blocks).  A QP's bits must not depend on the kernel instance or launch that solves it (one- or two-wave
+#     Riccati instance, the fused dense + Riccati launch); round 5 found the default broke that identity once the
+#     kernel bodies became shared device functions.  0.6-1.4 % faster on configs 2-5 (tools/ab_bench.sh).
+#   -fno-signed-zeros: lets the compiler drop additions of and multiplications into structural zeros of the unrolled
+#     lane patterns (x + 0.0 = x up to the sign of a zero result; nothing here reads a zero's sign, and NaNs still
+#     propagate to the NaN guard): config 4 9.74 -> 9.48 ms, config 5 3.33 -> 3.28 ms, config 2 within noise, every
+#     GPU test at its tolerance (profiles/r05/fused/ab_math_flags.log; -freciprocal-math gained < 1 %, not adopted).
+KERNEL_FP = ["-ffp-contract=on", "-fno-signed-zeros"]
 SCHED_FLAGS = {
     "lmpc_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-    "lmpc_dense.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + FP_CONTRACT,
-    "lmpc_lq.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + FP_CONTRACT,
+    "lmpc_dense.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + KERNEL_FP,
+    # the LDS Riccati kernel re-measured in round 5 (profiles/r05/fused/ab_sched.log): iterative-ilp config 4
+    # 9.46 -> 9.26 ms, config 5 3.29 -> 3.12 ms; the dense body prefers max-ilp (config 2 +1.2 % under iterative-ilp),
+    # so the fused dense + Riccati kernel has a file of its own
+    "lmpc_lq.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"] + KERNEL_FP,
+    "lmpc_fused.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + KERNEL_FP,
     "lmpc_gi.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
     "lmpc_hoqp.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
 
-SOURCES = ["lmpc_kernels.hip", "lmpc_lq.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
+SOURCES = ["lmpc_kernels.hip", "lmpc_lq.hip", "lmpc_fused.hip", "lmpc_dense.hip", "lmpc_gi.hip", "lmpc_prep.hip", "lmpc_hoqp.hip", "lmpc_wbc.hip", "lmpc_capi.cpp",
            "hoqp_capi.cpp", "lmpc_host.cpp", "ConvexQPSolver.cpp"]
-HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_dense_kernel.h",
+HEADERS = ["lmpc_device.h", "lmpc_common.h", "lmpc_kernel_common.h", "lmpc_dense_common.h", "lmpc_dense_kernel.h", "lmpc_lq_kernel.h",
            "lmpc_hoqp_device.h"]
 
 
@@ -141,10 +149,10 @@ TEST_BUILD = os.path.join(ROOT, "tests", "build")
 # kernel's forward sweep -- round 4's lost "+ za", and the next stage's yaw read for A_k -- with the polish's KKT
 # certificate (the product's verification) and without it (LMPC_KKT_OFF: round 4's verification).
 TEST_VARIANTS = {
-    "bugza": (["LMPC_BUG_ZA"], ("lmpc_lq.hip",)),
-    "bugza_nokkt": (["LMPC_BUG_ZA", "LMPC_KKT_OFF"], ("lmpc_lq.hip",)),
-    "bugyaw": (["LMPC_BUG_YAW"], ("lmpc_lq.hip",)),
-    "bugyaw_nokkt": (["LMPC_BUG_YAW", "LMPC_KKT_OFF"], ("lmpc_lq.hip",)),
+    "bugza": (["LMPC_BUG_ZA"], ("lmpc_lq.hip", "lmpc_fused.hip")),
+    "bugza_nokkt": (["LMPC_BUG_ZA", "LMPC_KKT_OFF"], ("lmpc_lq.hip", "lmpc_fused.hip")),
+    "bugyaw": (["LMPC_BUG_YAW"], ("lmpc_lq.hip", "lmpc_fused.hip")),
+    "bugyaw_nokkt": (["LMPC_BUG_YAW", "LMPC_KKT_OFF"], ("lmpc_lq.hip", "lmpc_fused.hip")),
 }
 
 

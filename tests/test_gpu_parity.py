@@ -541,6 +541,41 @@ def test_ipm_iteration_cap_hands_over_to_riccati(path, torch_dev):
     assert rel_err(gc, ref) <= TOL_REGRESS and rel_err(gd, ref) <= TOL_REGRESS
 
 
+@pytest.mark.parametrize("cid", [2, 4])
+def test_fused_launch_equals_two_launches(cid, torch_dev):
+    """At most one QP per SIMD (batch <= 4 x CUs) the device path runs the dense interior point and the Riccati
+    fallback as one launch (lmpc_dense_lq_kernel, round 5); one QP more and it launches the two kernels (the Riccati
+    one in its two-wave instance).  The QPs both batches share get the same bits: config 2 (every QP on the dense
+    path) and config 4's mixed gaits with terrain (a quarter dense-eligible, the rest solved by the Riccati body
+    inside the fused kernel)."""
+    import torch
+
+    cus = torch.cuda.get_device_properties(torch_dev).multi_processor_count
+    n = 4 * cus
+    p, H, rec, con = synth.config_batch(cid, count=n + 1)
+    nrm = synth.config_normals(cid, n + 1) if cid == 4 else None
+    s = BatchedConvexQPSolver(p, H, max_batch=0, dense_path="ipm")
+
+    def run(b):
+        out = torch.empty((b, H, 12), dtype=torch.float64, device=torch_dev)
+        st = torch.empty(b, dtype=torch.int32, device=torch_dev)
+        it = torch.empty(b, dtype=torch.int32, device=torch_dev)
+        d_nrm = None if nrm is None else torch.from_numpy(nrm[:b]).to(torch_dev).contiguous()
+        s.solve_device(torch.from_numpy(rec[:b]).to(torch_dev), torch.from_numpy(con[:b]).to(torch_dev), out, st, it,
+                       normals=d_nrm)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
+
+    g1, s1, i1 = run(n)      # fused
+    g2, s2, i2 = run(n + 1)  # two launches
+    assert np.all(s1 == 0) and np.all(s2 == 0)
+    assert np.array_equal(g1, g2[:n]) and np.array_equal(i1, i2[:n])
+    idx = np.random.default_rng(cid).choice(n, 16, replace=False)
+    ref, _, fails = O.solve_batch(O.params_from(p), H, rec[idx], con[idx], n_threads=8,
+                                  normals=None if nrm is None else nrm[idx])
+    assert fails == 0 and rel_err(g1[idx], ref) <= TOL
+
+
 def test_mixed_streams_and_host_path_share_one_context(torch_dev):
     """One context, three calls in flight: an asynchronous device solve on stream A (Riccati kernel: per-QP
     factor scratch), a host-pointer solve (the context's own stream, same scratch slots) issued before A has
