@@ -127,6 +127,19 @@ __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, doub
 // At two waves per SIMD the reduced stage reads its U row after the pivot staging and stores Z_k after the solve
 // (shorter live ranges across the 6 x 6 factor; the lone-wave instances keep the early read, 2 % faster there -- the
 // same arithmetic either way, so every instance gives the same bits); 0 = the early read everywhere (diagnostic)
+// 1 fences the next stage's operand fetch off from the machine scheduler (one block between the stage's first
+// matrix-core chain and its leg-block work: round 4's choice under max-ilp).  Under iterative-ilp (round 5) the
+// scheduler places it better on its own: configs 3/4/5 -1.7/-0.3/-1.6 % without the fence
+// (profiles/r05/fused/ab_lq_fence_hoist.log), so 0 is the default; 1 is kept for A/B.
+#ifndef LMPC_LQ_FETCH_FENCE
+#define LMPC_LQ_FETCH_FENCE 0
+#endif
+// 1 loads a serial-sweep stage's operands one stage ahead in the lone-wave instance (round 4).  Under iterative-ilp
+// (round 5) loading them in the stage is faster -- the second operand set's registers cost more than the load
+// latency they hid: config 2 --dense off -3 %, configs 3/5 -2 % (profiles/r05/fused/ab_lq_late_prefetch.log).
+#ifndef LMPC_LQ_PF
+#define LMPC_LQ_PF 0
+#endif
 #ifndef LMPC_LQ_LATE
 #define LMPC_LQ_LATE 1
 #endif
@@ -138,9 +151,12 @@ __device__ __forceinline__ int lq_opaque(int v) {
 }
 // The lane index for the lane-static operand maps of a phase: opaque at two waves per SIMD (recomputed where used:
 // 256 registers cannot hold them across the solve), plain in the lone-wave instance (512 registers: computed once).
+#ifndef LMPC_LQ_OPAQUE_W1
+#define LMPC_LQ_OPAQUE_W1 0
+#endif
 template <int WPE>
 __device__ __forceinline__ int lq_lane(int lane) {
-    return WPE == 1 ? lane : lq_opaque(lane);
+    return (WPE == 1 && !LMPC_LQ_OPAQUE_W1) ? lane : lq_opaque(lane);
 }
 
 // The same products branch-free for a runtime row r: (A x)[r] = x[r] + dt (a1 x[c1] + a2 x[c2]) and
@@ -229,9 +245,9 @@ __device__ __forceinline__ void lq_body(const DevParams prm, const double* __res
     const double* rin = rec + (size_t)qp * RL;
     const double* xr = rin + 33;  // x_ref (global, L2-resident after its first use)
     const double mu = prm.mu, fzmax = prm.fmax, dt = prm.dt;
-    // the serial sweeps load a stage's operands one stage ahead in the lone-wave instance (its latency is
-    // nobody else's to hide); at two waves per SIMD the second set of registers would spill instead
-    constexpr bool LQ_PF = WPE == 1;
+    // the serial sweeps can load a stage's operands one stage ahead in the lone-wave instance (LMPC_LQ_PF, off by
+    // default since round 5); at two waves per SIMD the second set of registers would spill
+    constexpr bool LQ_PF = LMPC_LQ_PF && WPE == 1;
     constexpr bool LQ_LATE = LQ_LATE_ON && WPE == 2;
     // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: measured -1.2 % on config 4 (stages
     // with three or four stance legs), +2.5 % on config 2 with the dense path off (a trot's full polish stage has only
@@ -855,9 +871,13 @@ __device__ __forceinline__ void lq_body(const DevParams prm, const double* __res
                         G = MFMA64(bh[0], C[1], G);
                         G = MFMA64(bh[1], C[2], G);
                         // next stage's operands, issued while the matrix cores work through the chain above
+#if LMPC_LQ_FETCH_FENCE
                         __builtin_amdgcn_sched_barrier(0);
+#endif
                         fetch(k > 0 ? k - 1 : 0);
+#if LMPC_LQ_FETCH_FENCE
                         __builtin_amdgcn_sched_barrier(0);
+#endif
                         // reduced inputs: this lane's U row (c = lc - 6, for its X columns), read before Z_k overwrites U_k
                         double ur[6];
                         auto read_ur = [&]() {
