@@ -393,6 +393,10 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
 struct DiagInv {
     d4 ui, uit;
 };
+// 1: the 3x3 pivot's reciprocals one after another instead of from the leading minors (diagnostic A/B)
+#ifndef LMPC_DIAG_SEQ_RSQ
+#define LMPC_DIAG_SEQ_RSQ 0
+#endif
 // Inlined at its call sites (round 3): outlined, the call cost the caller ~1.7 k cycles per tile in argument /
 // result moves and in the caller-saved registers it had to park around the call (5.6 k cycles per tile in the
 // kernel vs 3.9 k alone, tools/ubench/diag_parts.hip); inlined, config 2 runs 2 % faster (0.2304 -> 0.2259 ms,
@@ -443,6 +447,14 @@ static __device__ __attribute__((LMPC_DIAG_ATTR)) DiagInv diag_inverse(ldouble* 
         // P = L_p L_p' with the three pivot reciprocals from the leading minors, so their rsq chains run side by
         // side instead of one after the other: d1 = m11 / p00, d2 = det / m11 (m11 = p00 p11 - p10^2), hence
         // 1/sqrt(d1) = sqrt(p00) rsq(m11) and 1/sqrt(d2) = sqrt(m11) rsq(det)
+#if LMPC_DIAG_SEQ_RSQ
+        // the pivots one after another (12 fewer fp64 instructions, two more rsq latencies on the chain)
+        const double i00 = rsq_nr(p00);
+        const double l10 = p10 * i00, l20 = p20 * i00;
+        const double i11 = rsq_nr(fma(-l10, l10, p11));
+        const double l21 = fma(-l20, l10, p21) * i11;
+        const double i22 = rsq_nr(fma(-l21, l21, fma(-l20, l20, p22)));
+#else
         const double m11 = fma(p00, p11, -p10 * p10);
         const double c00 = fma(p11, p22, -p21 * p21), c01 = fma(p10, p22, -p21 * p20), c02 = fma(p10, p21, -p11 * p20);
         const double det = fma(p00, c00, fma(-p10, c01, p20 * c02));
@@ -451,6 +463,7 @@ static __device__ __attribute__((LMPC_DIAG_ATTR)) DiagInv diag_inverse(ldouble* 
         const double i11 = (p00 * i00) * r1;
         const double l21 = fma(-l20, l10, p21) * i11;
         const double i22 = (m11 * r1) * r2;
+#endif
         // row c of L_C (zero in and above the pivot rows)
         const double x0 = t0 * i00;
         const double x1 = fma(-l10, x0, t1) * i11;

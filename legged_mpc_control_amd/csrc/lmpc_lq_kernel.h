@@ -137,6 +137,10 @@ __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, doub
 // 1 loads a serial-sweep stage's operands one stage ahead in the lone-wave instance (round 4).  Under iterative-ilp
 // (round 5) loading them in the stage is faster -- the second operand set's registers cost more than the load
 // latency they hid: config 2 --dense off -3 %, configs 3/5 -2 % (profiles/r05/fused/ab_lq_late_prefetch.log).
+// reduced-input polish stages also at two leg-steps per lane (diagnostic A/B; see LQ_RP in the kernel)
+#ifndef LMPC_LQ_RP2
+#define LMPC_LQ_RP2 0
+#endif
 #ifndef LMPC_LQ_PF
 #define LMPC_LQ_PF 0
 #endif
@@ -252,7 +256,7 @@ __device__ __forceinline__ void lq_body(const DevParams prm, const double* __res
     // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: measured -1.2 % on config 4 (stages
     // with three or four stance legs), +2.5 % on config 2 with the dense path off (a trot's full polish stage has only
     // two pivot blocks); both instances alike, as kzs above; at two leg-steps per lane the leg-step work is not repaid
-    constexpr bool LQ_RP = LS == 1;
+    constexpr bool LQ_RP = LS == 1 || LMPC_LQ_RP2;
     LQ_STAMP_DECL
 
     // ---- prologue: record, terrain frames, I_w^-1, G0, yaw cos / sin ----------------------------------------
