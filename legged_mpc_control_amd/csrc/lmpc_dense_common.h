@@ -131,7 +131,8 @@ struct DSmem {
     ldouble* blk;   // 180: per-leg-step 3x3 block (D in the IPM, T in the polish)
     ldouble* act;   // 20: 1 = leg-step coupled (T != 0)
     ldouble* lup;   // 60: polish particular solution up per leg-step (kept out of registers)
-    ldouble* lua;   // 60: predictor step u_aff per leg-step
+    ldouble* lua;   // 64: predictor step u_aff per leg-step (interior point) | the last factorised polish round's
+                    //     solution y0 by variable (polish, range-space rounds: lmpc_dense_kernel.h)
     ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | diag_inverse: T, W staging (256) W' (272) | h_matvec (48)
     lint* lsm;      // 20: stance leg-step b -> 4k + j
     lint* fb;       // H+1: first stance leg-step of step k
@@ -153,7 +154,7 @@ __device__ __forceinline__ DSmem dcarve(double* sm, int H) {
     s.blk = p; p += 180;
     s.act = p; p += 20;
     s.lup = p; p += 60;
-    s.lua = p; p += 60;
+    s.lua = p; p += 64;
     s.cs = p; p += 2 * H;
     s.xr = p; p += 12 * H;
     s.em = p; p += 12 * H;

@@ -21,6 +21,15 @@
 #define DSTAMP_FLUSH(qp) do {} while (0)
 #endif
 
+// Range-space (Schur complement) polish rounds after a factorised one (dense_body): 1 on, 0 every round refactors;
+// LMPC_SCHUR_KMAX added face rows at most per update
+#ifndef LMPC_POLISH_SCHUR
+#define LMPC_POLISH_SCHUR 1
+#endif
+#ifndef LMPC_SCHUR_KMAX
+#define LMPC_SCHUR_KMAX 6
+#endif
+
 namespace lmpc {
 
 // ---------------------------------------------------------------------------
@@ -91,6 +100,14 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
     // factors (their M tiles, and every panel and update feeding them, are bitwise those of the previous round)
     int keep_tiles = 0;
     bool apex = false;
+    // Range-space polish rounds (LMPC_POLISH_SCHUR): a round whose active set only adds faces to the set of the last
+    // factorised round (bact, per leg-step lane) is that round's equality QP with k more rows A y = d on its
+    // coordinates y, so y = y0 - M^-1 A' (A M^-1 A')^-1 (A y0 - d) from the factorisation in hand: k + 1 solves and
+    // a k x k Cholesky instead of T'HT, its tiled Cholesky and one solve (tools/polish_schur_proto.py: 113 of 143
+    // later rounds qualify on config 2).  The verification below is the same either way.
+    int bact = 0;
+    bool have_base = false, schur = false;
+    int nsch = 0;
     double mu_c = 0.0, smu = 0.0, sz = 0.0;  // sz = sum of s'z at the iterate (mu_c = sz / mc)
     // factor tiles (register resident through the corrector): U's off-diagonal tiles in Tl, U_bb^-1, U_bb^-T
     d4 Tl[10], Ui[4], UiT[4];
@@ -133,6 +150,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
                 mode = POLISH;
                 rd = 0;
                 keep_tiles = 0;
+                have_base = false;
             } else {
                 double W[5] = {0, 0, 0, 0, 0}, wv[5] = {0, 0, 0, 0, 0};
                 if (st) {
@@ -154,14 +172,48 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             }
             DSTAMP(13);  // Newton-matrix blocks D and weights
         }
+        double Tn[9], upn[3];  // this polish round's leg basis (leg_basis of act)
         if (mode == POLISH) {
             ++prounds;
             apex = false;
-            double T[9], up[3];
-            if (st) apex = leg_basis(act, mu, fzmax, T, up);
+            double (&T)[9] = Tn;
+            if (st) apex = leg_basis(act, mu, fzmax, T, upn);
+            schur = false;
+#if LMPC_POLISH_SCHUR
+            if (have_base) {
+                // qualifies where every leg-step keeps its factorised faces and adds at most two, each removing one
+                // free direction of the factorised basis (independent of the faces it joins), none at the apex
+                const int add = st ? (act & ~bact) : 0;
+                const int k = __popc(add);
+                bool ok = !st || (act & bact) == bact;  // a dropped face (any leg-step) needs a factorisation
+                if (st && add) {
+                    const ldouble* Tb = S.blk + 9 * lane;
+                    int nb = 0, nn = 0;
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        nb += (Tb[q] != 0.0 || Tb[3 + q] != 0.0 || Tb[6 + q] != 0.0) ? 1 : 0;
+                        nn += (T[q] != 0.0 || T[3 + q] != 0.0 || T[6 + q] != 0.0) ? 1 : 0;
+                    }
+                    ok = ok && !apex && k <= 2 && nn == nb - k;
+                }
+                const unsigned long long b1 = __ballot(k >= 1), b2 = __ballot(k >= 2);
+                nsch = __popcll(b1) + __popcll(b2);
+                schur = __all(ok) && nsch >= 1 && nsch <= LMPC_SCHUR_KMAX;
+            }
+            // a factorised round: tiles ahead of the first leg-step whose faces differ from the last factorised
+            // round's keep their factors
+            if (!schur) {
+                const unsigned long long dif = __ballot(have_base && act != bact);
+                keep_tiles = have_base && dif ? (__ffsll((long long)dif) - 1) / 5 : 0;
+            }
+#endif
+        }
+        if (mode == POLISH && !schur) {
             S.vec2[lane] = 0.0;  // padding / unused variables of the up vector
             LMPC_SYNC();
             if (st) {
+                const double (&T)[9] = Tn;
+                const double (&up)[3] = upn;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) S.lup[3 * lane + p] = up[p];
                 ldouble* bk = S.blk + 9 * lane;
@@ -176,7 +228,8 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             }
         }
         // ---- right-hand side (and, except in the corrector, the Newton matrix) ----
-        if (mode != POLISH) {
+        if (schur) {
+        } else if (mode != POLISH) {
             if (st) {
 #pragma unroll
                 for (int a = 0; a < 3; ++a) S.vec[vidx(lane, a)] = -(S.gv[vidx(lane, a)] + rt[a]);
@@ -202,7 +255,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
         }
         if (mode == POLISH) DSTAMP(11);  // polish set-up + right-hand side (matvec)
         else DSTAMP(2);                  // interior point: leg-step work + right-hand side
-        if (mode != CORR) {
+        if (mode != CORR && !schur) {
             // ---- M tiles ----
             if (mode == PRED) {
 #pragma unroll
@@ -291,8 +344,8 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             }
         }
         DSTAMP(4);  // factorisation
-        // ---- solve: U'y = r, U x = y (vectors replicated across the accumulator columns) ----
-        {
+        // ---- solve: U'y = r, U x = y (vectors replicated across the accumulator columns), S.vec in place ----
+        auto solve_vec = [&]() {
             // forward: y_b = U_bb^-T (r_b - sum_{a<b} U_ab' y_a), all on the VALU (a matrix-core product would use
             // 1 of its 16 columns).  The bracket is column-indexed: lane 16g + c sums U_ab[4i+g][c] y_a[4i+g] over
             // its rows, then over the four row groups -> t[c]; y_b = UiT_b (r_b - t) row by row (the four
@@ -354,7 +407,121 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
                 }
             }
             LMPC_SYNC();
+        };
+        if (!schur) {
+            solve_vec();
+#if LMPC_POLISH_SCHUR
+            if (mode == POLISH) {  // this factorised round's solution and faces: the base of range-space rounds
+                S.lua[lane] = S.vec[lane];
+                bact = act;
+                have_base = true;
+            }
+#endif
         }
+#if LMPC_POLISH_SCHUR
+        else {
+            // ---- range-space round: y = y0 - W lambda, W = M^-1 A', (A W) lambda = A y0 - d ----
+            // rows of the added faces on the factorised coordinates (this lane's leg-step: T, up of the base)
+            const int add = st ? (act & ~bact) : 0;
+            const unsigned long long b1 = __ballot(__popc(add) >= 1), b2 = __ballot(__popc(add) >= 2);
+            const unsigned long long below = (1ull << lane) - 1ull;
+            const int r0 = __popcll(b1 & below) + __popcll(b2 & below);
+            ldouble* rows = S.scr + 64;                  // LMPC_SCHUR_KMAX x [a0 a1 a2 d]
+            ldouble* rleg = rows + 4 * LMPC_SCHUR_KMAX;  // leg-step of each row
+            ldouble* Wc = S.scr + 96;                    // M^-1 a_j by variable, 64 doubles each
+            if (add) {
+                const ldouble* Tb = S.blk + 9 * lane;
+                const ldouble* ub = S.lup + 3 * lane;
+                int r = r0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    if (!((add >> i) & 1)) continue;
+                    double c[3];
+                    cons_rowvec(i, mu, c);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) rows[4 * r + q] = fma(c[0], Tb[q], fma(c[1], Tb[3 + q], c[2] * Tb[6 + q]));
+                    rows[4 * r + 3] = (i == 4 ? fzmax : 0.0) - fma(c[0], ub[0], fma(c[1], ub[1], c[2] * ub[2]));
+                    rleg[r] = (double)lane;
+                    ++r;
+                }
+            }
+            LMPC_SYNC();
+            for (int j = 0; j < nsch; ++j) {  // wave-uniform
+                const int bj = (int)rleg[j];
+                S.vec[lane] = 0.0;
+                LMPC_SYNC();
+                if (lane < 3) S.vec[vidx(bj, lane)] = rows[4 * j + lane];
+                LMPC_SYNC();
+                solve_vec();
+                Wc[64 * j + lane] = S.vec[lane];
+            }
+            LMPC_SYNC();
+            // A W and A y0 - d on every lane, then its Cholesky (rows beyond nsch: identity)
+            constexpr int KM = LMPC_SCHUR_KMAX;
+            double Am[KM][KM], e[KM];
+#pragma unroll
+            for (int i = 0; i < KM; ++i) {
+                const bool iv = i < nsch;
+                const int bi = iv ? (int)rleg[i] : 0;
+                double a[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a[q] = iv ? rows[4 * i + q] : 0.0;
+                double ev = iv ? -rows[4 * i + 3] : 0.0;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) ev = fma(a[q], S.lua[vidx(bi, q)], ev);
+                e[i] = ev;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    double v = (!iv || j >= nsch) ? (i == j ? 1.0 : 0.0) : 0.0;
+                    if (iv && j < nsch) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) v = fma(a[q], Wc[64 * j + vidx(bi, q)], v);
+                    }
+                    Am[i][j] = v;
+                }
+            }
+            bool bad = false;
+#pragma unroll
+            for (int c = 0; c < KM; ++c) {
+                double d = Am[c][c];
+#pragma unroll
+                for (int b = 0; b < c; ++b) d = fma(-Am[c][b], Am[c][b], d);
+                bad |= !(d > 1e-14 * Am[c][c]);
+                const double inv = rsq_nr(d > 0.0 ? d : 1.0);
+                Am[c][c] = inv;  // the reciprocal of the pivot
+#pragma unroll
+                for (int r = c + 1; r < KM; ++r) {
+                    double v = Am[r][c];
+#pragma unroll
+                    for (int b = 0; b < c; ++b) v = fma(-Am[r][b], Am[c][b], v);
+                    Am[r][c] = v * inv;
+                }
+            }
+            double lam[KM];
+#pragma unroll
+            for (int r = 0; r < KM; ++r) {  // L w = e
+                double v = e[r];
+#pragma unroll
+                for (int b = 0; b < r; ++b) v = fma(-Am[r][b], lam[b], v);
+                lam[r] = v * Am[r][r];
+            }
+#pragma unroll
+            for (int r = KM - 1; r >= 0; --r) {  // L' lam = w
+                double v = lam[r];
+#pragma unroll
+                for (int b = r + 1; b < KM; ++b) v = fma(-Am[b][r], lam[b], v);
+                lam[r] = v * Am[r][r];
+            }
+            double yv = S.lua[lane];
+#pragma unroll
+            for (int j = 0; j < KM; ++j)
+                if (j < nsch) yv = fma(-Wc[64 * j + lane], lam[j], yv);
+            // a rank-deficient update (rounding): keep y0; the round will not verify and the next one refactors
+            S.vec[lane] = bad ? S.lua[lane] : yv;
+            if (bad) have_base = false;
+            LMPC_SYNC();
+        }
+#endif
         DSTAMP(5);  // solve
         // ---- leg-step solution ----
         u[0] = u[1] = u[2] = 0.0;
@@ -528,6 +695,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             keep_tiles = chg ? (__ffsll((long long)chg) - 1) / 5 : 0;  // tile of the first changed leg-step
             if (++rd >= prm.max_rounds) {
                 keep_tiles = 0;
+                schur = false;  // the interior point resumes: its own right-hand sides and factorisations
                 if (++att >= prm.max_attempts) break;
                 tol = retry_tol(tol, att);
                 it_end += prm.max_iter;
