@@ -5,7 +5,7 @@ import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from legged_mpc_control_amd import build as B
-os.environ["LMPC_LIB"] = B.build_stamps()
+os.environ["LMPC_LIB"] = os.environ.get("LMPC_STAMPS_LIB") or B.build_stamps()
 import numpy as np
 from legged_mpc_control_amd import BatchedConvexQPSolver, synth
 from legged_mpc_control_amd import _native as N
