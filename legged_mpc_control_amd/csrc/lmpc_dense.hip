@@ -104,7 +104,7 @@ extern "C" int lmpc_debug_dense_stamps(unsigned long long* out, int nqp) {
 
 size_t dense_lds_bytes(int H) {
     const int scr = 72 * H > DN_SCR_MIN ? 72 * H : DN_SCR_MIN;
-    const int doubles = 40 + 72 + 24 + 36 + 10 * DN_TILE + 64 * 3 + 180 + 20 + 60 + 64 + 2 * H + 12 * H + 12 * H + scr;
+    const int doubles = 40 + 72 + 24 + 36 + 10 * DN_TILE + 64 * 3 + 180 + 20 + 60 + 64 + 2 * H + 12 * H + 12 * H + 64 + scr;
     return (size_t)doubles * sizeof(double) + (20 + 33) * sizeof(int);
 }
 

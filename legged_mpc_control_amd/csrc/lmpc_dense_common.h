@@ -133,7 +133,9 @@ struct DSmem {
     ldouble* lup;   // 60: polish particular solution up per leg-step (kept out of registers)
     ldouble* lua;   // 64: predictor step u_aff per leg-step (interior point) | the last factorised polish round's
                     //     solution y0 by variable (polish, range-space rounds: lmpc_dense_kernel.h)
+    ldouble* lhg;   // 64: H up + g of the last factorised polish round (range-space rounds' new directions)
     ldouble* scr;   // union: P~ columns 6-11 (72H) during condensation | diag_inverse: T, W staging (256) W' (272) | h_matvec (48)
+                    //        | range-space rounds: h_matvec (48), entries (48..120), solves and column vectors (128..512)
     lint* lsm;      // 20: stance leg-step b -> 4k + j
     lint* fb;       // H+1: first stance leg-step of step k
 };
@@ -158,6 +160,7 @@ __device__ __forceinline__ DSmem dcarve(double* sm, int H) {
     s.cs = p; p += 2 * H;
     s.xr = p; p += 12 * H;
     s.em = p; p += 12 * H;
+    s.lhg = p; p += 64;
     s.scr = p; p += (72 * H > DN_SCR_MIN ? 72 * H : DN_SCR_MIN);
     lint* ip = (lint*)p;
     s.lsm = ip;

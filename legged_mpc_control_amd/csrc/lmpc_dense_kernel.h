@@ -29,8 +29,69 @@
 #ifndef LMPC_SCHUR_KMAX
 #define LMPC_SCHUR_KMAX 6
 #endif
+// ... including rounds that drop factorised faces (new columns: the bordered system); 0: only rounds that add faces
+// cost rule in half-units of one solve: 2 per entry, LMPC_SCHUR_CW2 more per column (its matvec), LMPC_SCHUR_SLOPE2
+// per diagonal tile a refactorisation would keep, at most LMPC_SCHUR_LIM2
+#ifndef LMPC_SCHUR_CW2
+#define LMPC_SCHUR_CW2 0
+#endif
+#ifndef LMPC_SCHUR_SLOPE2
+#define LMPC_SCHUR_SLOPE2 4
+#endif
+#ifndef LMPC_SCHUR_LIM2
+#define LMPC_SCHUR_LIM2 10
+#endif
+#ifndef LMPC_POLISH_BORDER
+#define LMPC_POLISH_BORDER 1
+#endif
 
 namespace lmpc {
+
+// nonzero columns of a leg basis (leg_basis puts them first)
+template <typename P>
+__device__ __forceinline__ int ncols3(const P* T) {
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) n += (T[q] != 0.0 || T[3 + q] != 0.0 || T[6 + q] != 0.0) ? 1 : 0;
+    return n;
+}
+// sum over the wave of k in 0..7, and its exclusive prefix (lanes in `below`)
+__device__ __forceinline__ int wave_count3(int k) {
+    return __popcll(__ballot(k & 1)) + 2 * __popcll(__ballot(k & 2)) + 4 * __popcll(__ballot(k & 4));
+}
+__device__ __forceinline__ int wave_prefix3(int k, unsigned long long below) {
+    return __popcll(__ballot(k & 1) & below) + 2 * __popcll(__ballot(k & 2) & below) +
+           4 * __popcll(__ballot(k & 4) & below);
+}
+
+// One leg-step of a range-space polish round (dense_body): faces act against the factorised round's bact (basis
+// Tb in LDS; Tn = leg_basis(act), nap its apex flag).  The kept faces cm = act & bact leave nc free directions,
+// nb of them the factorised ones: kc = nc - nb new columns, kr rows (the added faces, each removing one free
+// direction, or at a new apex the nc rows u = 0).  ok = false: the round refactorises.
+struct SchurLeg {
+    int kc, kr;
+    bool ok;
+};
+__device__ __forceinline__ SchurLeg schur_leg(bool chg, int act, int bact, bool nap, const ldouble* Tb,
+                                              const double Tn[9], double mu, double fzmax) {
+    SchurLeg r{0, 0, true};
+    if (!chg) return r;
+    const bool bap = (bact & 3) == 3 || (bact & 12) == 12;
+    if (bap && nap) return r;  // the force stays zero
+    const int cm = act & bact;
+    double Tc[9], uc[3];
+    (void)leg_basis(cm, mu, fzmax, Tc, uc);
+    const int nb = ncols3(Tb), nc = ncols3(Tc), nn = ncols3(Tn);
+    r.kc = nc - nb;
+    r.kr = nap ? nc : __popc(act & ~bact);
+    // the factorised particular solution must lie in the kept space: no f_max face at an apex on either side
+    r.ok = r.kc >= 0 && r.kc <= 3 && r.kr <= 3 && (!bap || !(cm & 16)) && (!nap || !((act | bact) & 16)) &&
+           (nap || nn == nc - r.kr);
+#if !LMPC_POLISH_BORDER
+    r.ok = r.ok && r.kc == 0 && !nap && !bap;
+#endif
+    return r;
+}
 
 // ---------------------------------------------------------------------------
 // The dense-path solve of QP blockIdx.x, one wave.  Returns false for a QP it leaves to the Riccati kernel (more
@@ -107,7 +168,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
     // later rounds qualify on config 2).  The verification below is the same either way.
     int bact = 0;
     bool have_base = false, schur = false;
-    int nsch = 0;
+    int nsch = 0, ncol = 0;  // range-space entries (columns + rows) and columns of the current round
     double mu_c = 0.0, smu = 0.0, sz = 0.0;  // sz = sum of s'z at the iterate (mu_c = sz / mc)
     // factor tiles (register resident through the corrector): U's off-diagonal tiles in Tl, U_bb^-1, U_bb^-T
     d4 Tl[10], Ui[4], UiT[4];
@@ -181,24 +242,19 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             schur = false;
 #if LMPC_POLISH_SCHUR
             if (have_base) {
-                // qualifies where every leg-step keeps its factorised faces and adds at most two, each removing one
-                // free direction of the factorised basis (independent of the faces it joins), none at the apex
-                const int add = st ? (act & ~bact) : 0;
-                const int k = __popc(add);
-                bool ok = !st || (act & bact) == bact;  // a dropped face (any leg-step) needs a factorisation
-                if (st && add) {
-                    const ldouble* Tb = S.blk + 9 * lane;
-                    int nb = 0, nn = 0;
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        nb += (Tb[q] != 0.0 || Tb[3 + q] != 0.0 || Tb[6 + q] != 0.0) ? 1 : 0;
-                        nn += (T[q] != 0.0 || T[3 + q] != 0.0 || T[6 + q] != 0.0) ? 1 : 0;
-                    }
-                    ok = ok && !apex && k <= 2 && nn == nb - k;
-                }
-                const unsigned long long b1 = __ballot(k >= 1), b2 = __ballot(k >= 2);
-                nsch = __popcll(b1) + __popcll(b2);
-                schur = __all(ok) && nsch >= 1 && nsch <= LMPC_SCHUR_KMAX;
+                // Per changed leg-step: the faces it keeps (cm) span a space of nc free directions holding the
+                // factorised basis's nb; the update adds kc = nc - nb of them as new columns (faces dropped) and kr
+                // rows (faces added, or at a new apex the nc rows u = 0), each row removing one free direction.
+                // Not at an apex with the f_max face (its particular solution is not in the kept space).
+                const SchurLeg sl = schur_leg(st && act != bact, act, bact, apex, S.blk + 9 * lane, T, mu, fzmax);
+                const int k = sl.kc + sl.kr;
+                nsch = wave_count3(k);
+                ncol = wave_count3(sl.kc);
+                // against a refactorisation from the first changed tile kt on (cheaper the later kt)
+                const unsigned long long dif = __ballot(st && act != bact);
+                const int kt = dif ? (__ffsll((long long)dif) - 1) / 5 : 4;
+                schur = __all(sl.ok) && nsch + ncol <= LMPC_SCHUR_KMAX &&
+                        2 * nsch + LMPC_SCHUR_CW2 * ncol + LMPC_SCHUR_SLOPE2 * kt <= LMPC_SCHUR_LIM2;
             }
             // a factorised round: tiles ahead of the first leg-step whose faces differ from the last factorised
             // round's keep their factors
@@ -241,6 +297,9 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             const double hv = h_matvec(S, S.vec2, S.scr, lane) + S.gv[lane];
             LMPC_SYNC();
             S.vec2[lane] = hv;
+#if LMPC_POLISH_SCHUR
+            S.lhg[lane] = hv;
+#endif
             LMPC_SYNC();
             if (st) {
 #pragma unroll
@@ -408,6 +467,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             }
             LMPC_SYNC();
         };
+        double du[3] = {0.0, 0.0, 0.0};  // range-space rounds: the new columns' part of this leg-step's force
         if (!schur) {
             solve_vec();
 #if LMPC_POLISH_SCHUR
@@ -420,102 +480,272 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
         }
 #if LMPC_POLISH_SCHUR
         else {
-            // ---- range-space round: y = y0 - W lambda, W = M^-1 A', (A W) lambda = A y0 - d ----
-            // rows of the added faces on the factorised coordinates (this lane's leg-step: T, up of the base)
-            const int add = st ? (act & ~bact) : 0;
-            const unsigned long long b1 = __ballot(__popc(add) >= 1), b2 = __ballot(__popc(add) >= 2);
+            // ---- range-space round on the factorised coordinates y (u_b = up_b + T_b y_b) ----
+            // Entries e < nsch, in leg-step order, a leg-step's columns before its rows:
+            //   column: a new free direction t (unit, in u-space) with coefficient w: v_e = T'H e_t (base
+            //           coordinates), c_e = -t'(H up + g)_b;
+            //   row:    r'u_b = beta on the base coordinates: v_e = T_b'r (on leg-step b only), c_e = beta - r'up_b.
+            // With W_e = M^-1 v_e and s = [w; lambda] the round's KKT system reduces to K s = c - V'y0,
+            // K = Cb - V'W (Cb: t't'H blocks between columns, r't between a row and a column of the same leg-step):
+            // quasi-definite (columns +, rows -), so LDL' needs no pivoting; y = y0 - W s, u_b += sum of t w.
+            constexpr int KM = LMPC_SCHUR_KMAX;
+            ldouble* U = S.scr + 48;       // KM x [x0 x1 x2 c]: t (column) or T_b'r (row), and c_e
+            ldouble* uleg = U + 4 * KM;    // leg-step of each entry
+            ldouble* utyp = uleg + KM;     // 0: row, 1 + j: column j
+            ldouble* Cb = utyp + KM;       // KM x KM
+            ldouble* Wc = S.scr + 128;     // M^-1 v_e by variable, 64 doubles each
+            ldouble* Vc = Wc + 64 * nsch;  // the columns' v_e by variable (nsch + ncol <= KM)
+            const SchurLeg sl = schur_leg(st && act != bact, act, bact, apex, S.blk + 9 * lane, Tn, mu, fzmax);
             const unsigned long long below = (1ull << lane) - 1ull;
-            const int r0 = __popcll(b1 & below) + __popcll(b2 & below);
-            ldouble* rows = S.scr + 64;                  // LMPC_SCHUR_KMAX x [a0 a1 a2 d]
-            ldouble* rleg = rows + 4 * LMPC_SCHUR_KMAX;  // leg-step of each row
-            ldouble* Wc = S.scr + 96;                    // M^-1 a_j by variable, 64 doubles each
-            if (add) {
+            const int e0 = wave_prefix3(sl.kc + sl.kr, below), c0 = wave_prefix3(sl.kc, below);
+            if (lane < KM * KM) Cb[lane] = 0.0;
+            LMPC_SYNC();
+            if (sl.kc + sl.kr) {
                 const ldouble* Tb = S.blk + 9 * lane;
                 const ldouble* ub = S.lup + 3 * lane;
-                int r = r0;
+                double Tc[9], uc[3];
+                (void)leg_basis(act & bact, mu, fzmax, Tc, uc);
+                // new directions: T_c's columns beyond span(T_b) (orthonormal)
+                double tv[3][3];
+                const int nb = ncols3(Tb);
+                if (nb == 0) {
 #pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    if (!((add >> i) & 1)) continue;
-                    double c[3];
-                    cons_rowvec(i, mu, c);
+                    for (int j = 0; j < 3; ++j)
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) rows[4 * r + q] = fma(c[0], Tb[q], fma(c[1], Tb[3 + q], c[2] * Tb[6 + q]));
-                    rows[4 * r + 3] = (i == 4 ? fzmax : 0.0) - fma(c[0], ub[0], fma(c[1], ub[1], c[2] * ub[2]));
-                    rleg[r] = (double)lane;
-                    ++r;
+                        for (int p = 0; p < 3; ++p) tv[j][p] = Tc[3 * p + j];
+                } else {
+                    double best = -1.0, rb[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        double r[3] = {Tc[q], Tc[3 + q], Tc[6 + q]};
+#pragma unroll
+                        for (int m = 0; m < 2; ++m) {  // T_b's columns (nb <= 2 where columns are added)
+                            const double pr = Tb[m] * r[0] + Tb[3 + m] * r[1] + Tb[6 + m] * r[2];
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) r[p] = fma(-pr, Tb[3 * p + m], r[p]);
+                        }
+                        const double n2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+                        if (n2 > best) {
+                            best = n2;
+                            rb[0] = r[0]; rb[1] = r[1]; rb[2] = r[2];
+                        }
+                    }
+                    const double in = rsq_nr(best > 0.0 ? best : 1.0);
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) tv[0][p] = rb[p] * in;
+                    // second (nb = 1, nc = 3): orthogonal to T_b's column and the first
+                    const double b0 = Tb[0], b1 = Tb[3], b2 = Tb[6];
+                    tv[1][0] = b1 * tv[0][2] - b2 * tv[0][1];
+                    tv[1][1] = b2 * tv[0][0] - b0 * tv[0][2];
+                    tv[1][2] = b0 * tv[0][1] - b1 * tv[0][0];
+                    tv[2][0] = tv[2][1] = tv[2][2] = 0.0;
+                }
+                // rows: added faces, or at a new apex T_c's columns (u_b = 0)
+                double rv[3][3], rbv[3];
+                if (apex) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) rv[j][p] = Tc[3 * p + j];
+                        rbv[j] = 0.0;
+                    }
+                } else {
+                    const ActiveRows ar = active_rows(act & ~bact);
+                    cons_rowvec(ar.i0, mu, rv[0]);
+                    cons_rowvec(ar.i1, mu, rv[1]);
+                    cons_rowvec(ar.i2, mu, rv[2]);
+                    rbv[0] = ar.i0 == 4 ? fzmax : 0.0;
+                    rbv[1] = ar.i1 == 4 ? fzmax : 0.0;
+                    rbv[2] = ar.i2 == 4 ? fzmax : 0.0;
+                }
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    if (j >= sl.kc) continue;
+                    const int e = e0 + j;
+                    double c = 0.0;
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        U[4 * e + p] = tv[j][p];
+                        c = fma(-tv[j][p], S.lhg[vidx(lane, p)], c);
+                    }
+                    U[4 * e + 3] = c;
+                    uleg[e] = (double)lane;
+                    utyp[e] = (double)(1 + c0 + j);
+                }
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (i >= sl.kr) continue;
+                    const int e = e0 + sl.kc + i;
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        U[4 * e + q] = fma(rv[i][0], Tb[q], fma(rv[i][1], Tb[3 + q], rv[i][2] * Tb[6 + q]));
+                    U[4 * e + 3] = rbv[i] - fma(rv[i][0], ub[0], fma(rv[i][1], ub[1], rv[i][2] * ub[2]));
+                    uleg[e] = (double)lane;
+                    utyp[e] = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        if (j >= sl.kc) continue;
+                        const double a = rv[i][0] * tv[j][0] + rv[i][1] * tv[j][1] + rv[i][2] * tv[j][2];
+                        Cb[KM * e + e0 + j] = a;
+                        Cb[KM * (e0 + j) + e] = a;
+                    }
                 }
             }
             LMPC_SYNC();
-            for (int j = 0; j < nsch; ++j) {  // wave-uniform
-                const int bj = (int)rleg[j];
-                S.vec[lane] = 0.0;
-                LMPC_SYNC();
-                if (lane < 3) S.vec[vidx(bj, lane)] = rows[4 * j + lane];
+            // columns: v = T'H e_t (one matvec each), and the t't'H block of Cb
+            if (ncol) {
+                const int w16 = lane & 15, bl = 5 * (lane >> 4) + w16 / 3, al = w16 % 3;
+                const bool vl = w16 < 15 && bl < nls;
+                for (int e = 0; e < nsch; ++e) {  // wave-uniform
+                    const double ty = utyp[e];
+                    if (ty < 0.5) continue;
+                    const int be = (int)uleg[e];
+                    S.vec2[lane] = 0.0;
+                    LMPC_SYNC();
+                    if (lane < 3) S.vec2[vidx(be, lane)] = U[4 * e + lane];
+                    LMPC_SYNC();
+                    const double h = h_matvec(S, S.vec2, S.scr, lane);
+                    LMPC_SYNC();
+                    S.vec2[lane] = h;
+                    LMPC_SYNC();
+                    double v = 0.0;
+                    if (vl) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) v = fma(S.blk[9 * bl + 3 * p + al], S.vec2[vidx(bl, p)], v);
+                    }
+                    Vc[64 * ((int)ty - 1) + lane] = v;
+                    if (lane < nsch && utyp[lane] > 0.5) {
+                        const int bj = (int)uleg[lane];
+                        double c = 0.0;
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) c = fma(U[4 * lane + p], S.vec2[vidx(bj, p)], c);
+                        Cb[KM * lane + e] = c;
+                    }
+                    LMPC_SYNC();
+                }
+            }
+            // W_e = M^-1 v_e
+            for (int e = 0; e < nsch; ++e) {  // wave-uniform
+                const double ty = utyp[e];
+                if (ty > 0.5) {
+                    S.vec[lane] = Vc[64 * ((int)ty - 1) + lane];
+                } else {
+                    S.vec[lane] = 0.0;
+                    LMPC_SYNC();
+                    if (lane < 3) S.vec[vidx((int)uleg[e], lane)] = U[4 * e + lane];
+                }
                 LMPC_SYNC();
                 solve_vec();
-                Wc[64 * j + lane] = S.vec[lane];
+                Wc[64 * e + lane] = S.vec[lane];
             }
             LMPC_SYNC();
-            // A W and A y0 - d on every lane, then its Cholesky (rows beyond nsch: identity)
-            constexpr int KM = LMPC_SCHUR_KMAX;
-            double Am[KM][KM], e[KM];
+            // column-column products and the columns' right-hand sides (wave sums over the variables)
+            if (ncol) {
+                const double y0l = S.lua[lane];
+                for (int e = 0; e < nsch; ++e) {  // wave-uniform
+                    const double ty = utyp[e];
+                    if (ty < 0.5) continue;
+                    const double vl = Vc[64 * ((int)ty - 1) + lane];
+                    const double cy = wave_sum(vl * y0l);
+                    if (lane == 0) U[4 * e + 3] -= cy;
+                    for (int f = e; f < nsch; ++f) {
+                        if (utyp[f] < 0.5) continue;
+                        const double g = wave_sum(vl * Wc[64 * f + lane]);
+                        if (lane == 0) {
+                            Cb[KM * e + f] -= g;
+                            if (f != e) Cb[KM * f + e] -= g;
+                        }
+                    }
+                }
+                LMPC_SYNC();
+            }
+            // K and its right-hand side on every lane (entries beyond nsch: identity); rows by their 3 entries
+            double Am[KM][KM], cv[KM], sg[KM];
+            int rb_[KM];
+            bool rw[KM];
 #pragma unroll
             for (int i = 0; i < KM; ++i) {
                 const bool iv = i < nsch;
-                const int bi = iv ? (int)rleg[i] : 0;
+                rw[i] = iv && utyp[iv ? i : 0] < 0.5;
+                rb_[i] = iv ? (int)uleg[i] : 0;
+                sg[i] = rw[i] ? -1.0 : 1.0;
+            }
+#pragma unroll
+            for (int i = 0; i < KM; ++i) {
+                const bool iv = i < nsch;
                 double a[3];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) a[q] = iv ? rows[4 * i + q] : 0.0;
-                double ev = iv ? -rows[4 * i + 3] : 0.0;
+                for (int q = 0; q < 3; ++q) a[q] = rw[i] ? U[4 * i + q] : 0.0;
+                double c = iv ? U[4 * i + 3] : 0.0;
+                if (rw[i]) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q) ev = fma(a[q], S.lua[vidx(bi, q)], ev);
-                e[i] = ev;
+                    for (int q = 0; q < 3; ++q) c = fma(-a[q], S.lua[vidx(rb_[i], q)], c);
+                }
+                cv[i] = c;
 #pragma unroll
-                for (int j = 0; j < KM; ++j) {
-                    double v = (!iv || j >= nsch) ? (i == j ? 1.0 : 0.0) : 0.0;
-                    if (iv && j < nsch) {
+                for (int j = 0; j <= i; ++j) {
+                    const bool jv = j < nsch;
+                    double v = (iv && jv) ? Cb[KM * i + j] : (i == j ? 1.0 : 0.0);
+                    if (iv && jv) {
+                        if (rw[i]) {
 #pragma unroll
-                        for (int q = 0; q < 3; ++q) v = fma(a[q], Wc[64 * j + vidx(bi, q)], v);
+                            for (int q = 0; q < 3; ++q) v = fma(-a[q], Wc[64 * j + vidx(rb_[i], q)], v);
+                        } else if (rw[j]) {
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) v = fma(-U[4 * j + q], Wc[64 * i + vidx(rb_[j], q)], v);
+                        }
                     }
                     Am[i][j] = v;
                 }
             }
+            // L D L' (lower triangle; D in dd)
             bool bad = false;
+            double dd[KM];
 #pragma unroll
             for (int c = 0; c < KM; ++c) {
                 double d = Am[c][c];
 #pragma unroll
-                for (int b = 0; b < c; ++b) d = fma(-Am[c][b], Am[c][b], d);
-                bad |= !(d > 1e-14 * Am[c][c]);
-                const double inv = rsq_nr(d > 0.0 ? d : 1.0);
-                Am[c][c] = inv;  // the reciprocal of the pivot
+                for (int b = 0; b < c; ++b) d = fma(-Am[c][b], Am[c][b] * dd[b], d);
+                bad |= !(sg[c] * d > 1e-14 * fabs(Am[c][c]));
+                dd[c] = d;
+                const double inv = rcp_nr(d != 0.0 ? d : 1.0);
 #pragma unroll
                 for (int r = c + 1; r < KM; ++r) {
                     double v = Am[r][c];
 #pragma unroll
-                    for (int b = 0; b < c; ++b) v = fma(-Am[r][b], Am[c][b], v);
+                    for (int b = 0; b < c; ++b) v = fma(-Am[r][b], Am[c][b] * dd[b], v);
                     Am[r][c] = v * inv;
                 }
             }
-            double lam[KM];
+            double sv[KM];
 #pragma unroll
-            for (int r = 0; r < KM; ++r) {  // L w = e
-                double v = e[r];
+            for (int r = 0; r < KM; ++r) {  // L z = c
+                double v = cv[r];
 #pragma unroll
-                for (int b = 0; b < r; ++b) v = fma(-Am[r][b], lam[b], v);
-                lam[r] = v * Am[r][r];
+                for (int b = 0; b < r; ++b) v = fma(-Am[r][b], sv[b], v);
+                sv[r] = v;
             }
 #pragma unroll
-            for (int r = KM - 1; r >= 0; --r) {  // L' lam = w
-                double v = lam[r];
+            for (int r = 0; r < KM; ++r) sv[r] = sv[r] * rcp_nr(dd[r] != 0.0 ? dd[r] : 1.0);
 #pragma unroll
-                for (int b = r + 1; b < KM; ++b) v = fma(-Am[b][r], lam[b], v);
-                lam[r] = v * Am[r][r];
+            for (int r = KM - 1; r >= 0; --r) {  // L' s = D^-1 z
+                double v = sv[r];
+#pragma unroll
+                for (int b = r + 1; b < KM; ++b) v = fma(-Am[b][r], sv[b], v);
+                sv[r] = v;
             }
             double yv = S.lua[lane];
 #pragma unroll
             for (int j = 0; j < KM; ++j)
-                if (j < nsch) yv = fma(-Wc[64 * j + lane], lam[j], yv);
+                if (j < nsch) yv = fma(-Wc[64 * j + lane], sv[j], yv);
+            if (ncol && !bad && st) {
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    if (j >= nsch || rw[j] || rb_[j] != lane) continue;
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) du[p] = fma(U[4 * j + p], sv[j], du[p]);
+                }
+            }
             // a rank-deficient update (rounding): keep y0; the round will not verify and the next one refactors
             S.vec[lane] = bad ? S.lua[lane] : yv;
             if (bad) have_base = false;
@@ -533,7 +763,9 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
                 const ldouble* Tb = S.blk + 9 * lane;
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
-                    u[p] = S.lup[3 * lane + p] + Tb[p * 3] * y3[0] + Tb[p * 3 + 1] * y3[1] + Tb[p * 3 + 2] * y3[2];
+                    u[p] = apex ? 0.0
+                                : S.lup[3 * lane + p] + Tb[p * 3] * y3[0] + Tb[p * 3 + 1] * y3[1] + Tb[p * 3 + 2] * y3[2] +
+                                      du[p];
             } else {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) u[p] = y3[p];

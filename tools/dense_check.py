@@ -81,6 +81,8 @@ def stamps():
         v = buf[:n, i].astype(float).mean()
         print(f"  {nm:20s} {v:10.0f} ({100 * v / tot.mean():5.1f}%)")
     print(f"  max cycles/QP {tot.max():.0f}, p99 {np.percentile(tot, 99):.0f}")
+    if os.environ.get("LMPC_STAMPS_OUT"):  # per-QP phase cycles and iteration words, for comparing builds
+        np.savez(os.environ["LMPC_STAMPS_OUT"], stamps=buf[:n], iters=it[:n])
     for q in np.argsort(-tot)[:6]:
         print(f"    slow QP {q}: {tot[q]:.0f} cycles, ipm {it[q] & 0xffff} rounds {it[q] >> 16}, "
               f"diag {buf[q, 6]:.0f} solve {buf[q, 5]:.0f}")
@@ -123,7 +125,7 @@ def gi_stamps():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "stamps":
         from legged_mpc_control_amd import build as B
-        os.environ["LMPC_LIB"] = B.build_stamps()
+        os.environ["LMPC_LIB"] = os.environ.get("LMPC_STAMPS_LIB") or B.build_stamps()
         ti = stamps()
         tg = gi_stamps()
         both = np.minimum(ti, tg)
