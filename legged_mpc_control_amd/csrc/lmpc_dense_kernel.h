@@ -41,6 +41,10 @@
 #ifndef LMPC_SCHUR_LIM2
 #define LMPC_SCHUR_LIM2 10
 #endif
+// interior-point start: z = LMPC_DENSE_Z0 / s (complementarity LMPC_DENSE_Z0 per pair)
+#ifndef LMPC_DENSE_Z0
+#define LMPC_DENSE_Z0 1.0
+#endif
 #ifndef LMPC_POLISH_BORDER
 #define LMPC_POLISH_BORDER 1
 #endif
@@ -144,8 +148,8 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
             s[i] = st ? -o[i] : 1.0;
-            z[i] = 1.0 / s[i];
-            is[i] = z[i];
+            is[i] = 1.0 / s[i];
+            z[i] = LMPC_DENSE_Z0 * is[i];
         }
     }
     double u[3] = {0.0, 0.0, 0.0}, rt[3] = {0.0, 0.0, 0.0};
