@@ -181,6 +181,13 @@ __device__ unsigned long long lmpc_condense_stamps[4096][5];
 #define CSTAMP(i) do {} while (0)
 #define CSTAMP_DECL
 #endif
+// 1: the H-column pass keeps G0's rows 0-2 in registers on flat ground (round 5: H columns 21.3 k -> 17.1 k cycles
+// per QP, config 2 -0.7 %, profiles/r05/border/ab_hoist_g0.log); 0: LDS loads in the loop (the compiler cannot hoist
+// them past the H stores, which may alias).  Loading the step's yaw terms one iteration ahead here and in the free
+// response changed neither phase's cycles and was not kept.
+#ifndef LMPC_COND_HOIST_G0
+#define LMPC_COND_HOIST_G0 1
+#endif
 template <bool TERRAIN>
 __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem& S, int H, int nls,
                                                unsigned long long smask, int lane) {
@@ -332,6 +339,17 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
             }
         }
         const int vkk = vvalid ? vk : -1;  // padding / unused lanes take part in no step
+#if LMPC_COND_HOIST_G0
+        // flat ground: rows 0-2 of G0 in registers (loop-invariant; in the loop they are LDS loads the compiler cannot
+        // hoist past the H stores, which may alias)
+        double g0r[3][12];
+        if constexpr (!TERRAIN) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+                for (int c = 0; c < 12; ++c) g0r[q][c] = S.G0[q * 12 + c];
+        }
+#endif
         for (int i = H - 1; i >= 0; --i) {
             if (i < vkk) {  // L <- A_{i+1}' L
                 const double ck = S.cs[2 * (i + 1)], sk = S.cs[2 * (i + 1) + 1];
@@ -359,8 +377,13 @@ __device__ __forceinline__ void dense_condense(const DevParams& prm, const DSmem
 #pragma unroll
                             for (int q = 0; q < 6; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
                         } else {  // flat ground: rows 3-5 of G0 are dt/m I (dense_prologue) -- the same sum, bit for bit
+#if LMPC_COND_HOIST_G0
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) val = fma(g0r[q][cp], L[6 + q], val);
+#else
 #pragma unroll
                             for (int q = 0; q < 3; ++q) val = fma(S.G0[q * 12 + cp], L[6 + q], val);
+#endif
                             val = fma(dtm, L[9 + ap], val);
                         }
                         if (bp == vb) val += rbl[ap];
