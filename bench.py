@@ -283,6 +283,7 @@ def main():
             reps += 1
             done_qps += ns
         ct = time.perf_counter() - t1
+        du0 = np.max(np.abs(g_admm[:, 0, :] - ref[:ns, 0, :]), axis=1)
         cpu = {
             "value": done_qps / ct,
             "unit": "QP/s",
@@ -296,6 +297,11 @@ def main():
             "admm_iters_mean": float(np.mean(it_admm)),
             "admm_converged": int(np.sum(cv_admm)),
             "max_abs_dev_from_exact_optimum_N": float(np.max(np.abs(g_admm - ref[:ns]))) if world == 1 else None,
+            # what the reference's tick consumes: u0 only (ConvexQPSolver.cpp:320-322) -- per QP max |du0| over its 12
+            # forces, against the exact optimum this build returns
+            "max_abs_dev_u0_N": float(np.max(du0)),
+            "p50_abs_dev_u0_N": float(np.percentile(du0, 50)),
+            "p99_abs_dev_u0_N": float(np.percentile(du0, 99)),
             "host": cpu_info,
         }
         # (2) the exact-optimum oracle (dense Goldfarb-Idnani), the parity checker, over the whole batch
@@ -420,6 +426,12 @@ def main():
             "ipm_iters_max": int(np.max(it & 0xFFFF)),
             "polish_rounds_max": int(np.max(it >> 16)),
             "ipm_iters_p99": float(np.percentile(it & 0xFFFF, 99)),
+            "polish_rounds_p99": float(np.percentile(it >> 16, 99)),
+            # per-QP iteration words of the measured batch (rank 0's shard): the launch waits for its slowest QP
+            "iteration_histogram": {
+                "ipm_iters": {str(k): int(v) for k, v in zip(*np.unique(it & 0xFFFF, return_counts=True))},
+                "polish_rounds": {str(k): int(v) for k, v in zip(*np.unique(it >> 16, return_counts=True))},
+            },
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

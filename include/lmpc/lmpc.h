@@ -66,10 +66,14 @@ extern "C" {
 #define LMPC_ERR_NOT_BUILT (-5)
 
 /* per-QP status codes (status[b]).  LMPC_QP_CONVERGED is a KKT certificate (ABI 7): the returned forces are primal
- * feasible (pyramid and bound rows within tol_p * f_max), the state trajectory the solver used is their dynamics
- * (x_{k+1} = A_k x_k + B u_k - g dt e11 within tol_x of the state scale), and along it the gradient has no component
- * on any stance leg-step's free directions (within tol_d of the gradient scale) and non-negative multipliers on its
- * active faces -- i.e. the exact optimum of the reference's QP to those tolerances. */
+ * feasible (pyramid and bound rows within tol_p * f_max), the gradient has no component on any stance leg-step's free
+ * directions (within tol_d of the gradient scale) and the multipliers of its active faces are non-negative -- i.e. the
+ * exact optimum of the reference's QP to those tolerances.  Which gradient depends on the kernel that solved the QP:
+ *   - the Riccati kernels (LMPC_DENSE_OFF, and every QP the dense paths leave) take it from the adjoint of the state
+ *     trajectory they swept, so they also check that this trajectory is the dynamics of the returned forces
+ *     (x_{k+1} = A_k x_k + B u_k - g dt e11 within tol_x of the state scale);
+ *   - the condensed dense paths (LMPC_DENSE_IPM, LMPC_DENSE_GI) take it as H u + g of the condensed QP, where the
+ *     dynamics hold by the construction of H and g (there is no trajectory to check): tol_x does not apply to them. */
 #define LMPC_QP_CONVERGED 0
 #define LMPC_QP_MAX_ITER 1 /* no certified optimum: the best (feasible) interior-point iterate returned */
 #define LMPC_QP_NAN 2      /* zeros returned, as the reference does (ConvexQPSolver.cpp:321-326) */
@@ -113,7 +117,7 @@ typedef struct lmpc_options {
     int warm_rounds;       /* warm start: polish rounds before the cold fallback (default 12) */
     /* ABI 7: the certificate's dynamics check -- the Riccati kernels' state trajectory against the dynamics of the
      * forces they return, relative to max(1, max |x|) (default 1e-8; the measured rounding level is <= 2e-10,
-     * DESIGN.md 2.6) */
+     * DESIGN.md 2.6).  The Riccati kernels only: the condensed dense paths have no trajectory (LMPC_QP_CONVERGED). */
     double tol_x;
 } lmpc_options;
 

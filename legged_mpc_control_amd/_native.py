@@ -296,11 +296,10 @@ def lib():
         L.lmpc_wbc_tasks.restype = ctypes.c_int
         L.lmpc_wbc_tasks_device.argtypes = [vp, ctypes.c_int, vp, vp]
         L.lmpc_wbc_tasks_device.restype = ctypes.c_int
-        # a diagnostic build of the previous round's sources (tools/ab_bench.sh A/B against it) may be one ABI behind:
-        # the bench path it runs (device commands, records, solve) does not depend on the ABI-7 layouts
-        ok = (ABI_VERSION - 1, ABI_VERSION) if os.environ.get("LMPC_LIB") else (ABI_VERSION,)
-        if L.lmpc_abi_version() not in ok:
-            raise NativeLibraryError("liblmpc.so ABI version mismatch")
+        # exactly this ABI, diagnostic builds (LMPC_LIB) included: the command and options structs above are ABI-7
+        # layouts, and an older library would read their fields at the wrong offsets without an error
+        if L.lmpc_abi_version() != ABI_VERSION:
+            raise NativeLibraryError(f"{path}: ABI version {L.lmpc_abi_version()}, this binding is ABI {ABI_VERSION}")
         _lib = L
         return L
 

@@ -153,6 +153,9 @@ TEST_VARIANTS = {
     "bugza_nokkt": (["LMPC_BUG_ZA", "LMPC_KKT_OFF"], ("lmpc_lq.hip", "lmpc_fused.hip")),
     "bugyaw": (["LMPC_BUG_YAW"], ("lmpc_lq.hip", "lmpc_fused.hip")),
     "bugyaw_nokkt": (["LMPC_BUG_YAW", "LMPC_KKT_OFF"], ("lmpc_lq.hip", "lmpc_fused.hip")),
+    # the dense polish with every round refactorised (no range-space updates): tests/test_gpu_kkt.py checks that the
+    # product's updates reach the same iteration words and forces
+    "noschur": (["LMPC_POLISH_SCHUR=0"], ("lmpc_dense.hip", "lmpc_lq.hip", "lmpc_fused.hip")),
 }
 
 

@@ -69,6 +69,21 @@ extern "C" int lmpc_debug_kkt_dense_clear(void) {
 }
 #endif
 
+#ifdef LMPC_REFINE_DIAG
+// diagnostic build (tools/refine_diag.py): per QP whose verified round was a range-space one, [stationarity residual
+// / gscale, K's smallest pivot ratio, max |refinement correction|, 1 accepted / 2 rejected]
+__device__ double lmpc_refine_diag[LMPC_KKT_DIAG_QPS][4];
+extern "C" int lmpc_debug_refine(double* out, int nqp) {
+    if (nqp > LMPC_KKT_DIAG_QPS) nqp = LMPC_KKT_DIAG_QPS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_refine_diag), (size_t)nqp * 4 * sizeof(double)) == hipSuccess
+               ? nqp : -1;
+}
+extern "C" int lmpc_debug_refine_clear(void) {
+    static double zeros[LMPC_KKT_DIAG_QPS * 4];
+    return hipMemcpyToSymbol(HIP_SYMBOL(lmpc_refine_diag), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 }  // namespace lmpc
 
 #include "lmpc_dense_kernel.h"

@@ -48,8 +48,29 @@
 #ifndef LMPC_POLISH_BORDER
 #define LMPC_POLISH_BORDER 1
 #endif
+// one step of iterative refinement of a verified range-space round whose stationarity residual is above
+// LMPC_REFINE_SR of the gradient scale, certified again (round 6); 0: the update as is.  Over 8192 config-2 QPs
+// (tools/refine_diag.py, profiles/r06/refine/) 1857 end on a range-space round; their residuals are <= 6.2e-13 of
+// gscale except one at 3.4e-12 -- the QP whose forces sat 1.8e-9 from the optimum (the others' corrections <= 3e-10).
+// Refining every such QP cost config 2 +3.4 %; this trigger refines that one.
+#ifndef LMPC_POLISH_REFINE
+#define LMPC_POLISH_REFINE 1
+#endif
+#ifndef LMPC_REFINE_SR
+#ifdef LMPC_REFINE_DIAG
+#define LMPC_REFINE_SR 0.0
+#else
+#define LMPC_REFINE_SR 1e-12
+#endif
+#endif
 
 namespace lmpc {
+
+// range-space rounds' scratch (S.scr): h_matvec 0..47, entries U / uleg / utyp / Cb 48..119, the round's s 120..125
+// (for its refinement) and K's smallest pivot ratio 126, W = M^-1 V and the columns' V from 128
+static_assert(48 + 4 * LMPC_SCHUR_KMAX + 2 * LMPC_SCHUR_KMAX + LMPC_SCHUR_KMAX * LMPC_SCHUR_KMAX <= 120 &&
+                  120 + LMPC_SCHUR_KMAX + 1 <= 128, "range-space scratch layout");
+constexpr int DN_SCHUR_SV = 120;
 
 // nonzero columns of a leg basis (leg_basis puts them first)
 template <typename P>
@@ -191,6 +212,87 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             if (r == lc) ldg_reg = i;
         }
     }
+#if LMPC_POLISH_SCHUR
+    // K s = cv of a range-space round (S.scr: entries U / uleg / utyp / Cb, W = M^-1 V in Wc; every lane alike):
+    // K = Cb - V'W, rows by their three entries, entries beyond nsch the identity; L D L' without pivoting (K is
+    // quasi-definite: columns +, rows -).  Returns true (bad) when a pivot leaves its sign: rank-deficient in rounding.
+    auto schur_ksolve = [&](const double (&cv)[LMPC_SCHUR_KMAX], double (&sv)[LMPC_SCHUR_KMAX], double& kmin) -> bool {
+        constexpr int KM = LMPC_SCHUR_KMAX;
+        const ldouble* U = S.scr + 48;
+        const ldouble* uleg = U + 4 * KM;
+        const ldouble* utyp = uleg + KM;
+        const ldouble* Cb = utyp + KM;
+        const ldouble* Wc = S.scr + 128;
+        double Am[KM][KM], sg[KM];
+        int rb_[KM];
+        bool rw[KM];
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {
+            const bool iv = i < nsch;
+            rw[i] = iv && utyp[iv ? i : 0] < 0.5;
+            rb_[i] = iv ? (int)uleg[i] : 0;
+            sg[i] = rw[i] ? -1.0 : 1.0;
+        }
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {
+            const bool iv = i < nsch;
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                const bool jv = j < nsch;
+                double v = (iv && jv) ? Cb[KM * i + j] : (i == j ? 1.0 : 0.0);
+                if (iv && jv) {
+                    if (rw[i]) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) v = fma(-U[4 * i + q], Wc[64 * j + vidx(rb_[i], q)], v);
+                    } else if (rw[j]) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) v = fma(-U[4 * j + q], Wc[64 * i + vidx(rb_[j], q)], v);
+                    }
+                }
+                Am[i][j] = v;
+            }
+        }
+        bool bad = false;
+        double dd[KM];
+#pragma unroll
+        for (int c = 0; c < KM; ++c) {
+            double d = Am[c][c];
+#pragma unroll
+            for (int b = 0; b < c; ++b) d = fma(-Am[c][b], Am[c][b] * dd[b], d);
+            bad |= !(sg[c] * d > 1e-14 * fabs(Am[c][c]));
+            if (c < nsch) kmin = fmin(kmin, fabs(d) / fabs(Am[c][c]));  // pivot over its diagonal: K's cancellation
+            dd[c] = d;
+            const double inv = rcp_nr(d != 0.0 ? d : 1.0);
+#pragma unroll
+            for (int r = c + 1; r < KM; ++r) {
+                double v = Am[r][c];
+#pragma unroll
+                for (int b = 0; b < c; ++b) v = fma(-Am[r][b], Am[c][b] * dd[b], v);
+                Am[r][c] = v * inv;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < KM; ++r) {  // L z = c
+            double v = cv[r];
+#pragma unroll
+            for (int b = 0; b < r; ++b) v = fma(-Am[r][b], sv[b], v);
+            sv[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < KM; ++r) sv[r] = sv[r] * rcp_nr(dd[r] != 0.0 ? dd[r] : 1.0);
+#pragma unroll
+        for (int r = KM - 1; r >= 0; --r) {  // L' s = D^-1 z
+            double v = sv[r];
+#pragma unroll
+            for (int b = r + 1; b < KM; ++b) v = fma(-Am[b][r], sv[b], v);
+            sv[r] = v;
+        }
+        return bad;
+    };
+    // a settled active set failed the certificate right after a range-space round: the same faces once more as a
+    // factorised round before the retry ladder (the update's rounding, not the faces, may be what failed)
+    bool force_fact = false, refact_done = false;
+#endif
     for (;;) {
         if (mode == PRED) {
             if (ipm_it >= prm.dense_iter_cap) break;  // test hook: hand the QP to the Riccati kernel
@@ -245,7 +347,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             if (st) apex = leg_basis(act, mu, fzmax, T, upn);
             schur = false;
 #if LMPC_POLISH_SCHUR
-            if (have_base) {
+            if (have_base && !force_fact) {
                 // Per changed leg-step: the faces it keeps (cm) span a space of nc free directions holding the
                 // factorised basis's nb; the update adds kc = nc - nb of them as new columns (faces dropped) and kr
                 // rows (faces added, or at a new apex the nc rows u = 0), each row removing one free direction.
@@ -265,6 +367,7 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             if (!schur) {
                 const unsigned long long dif = __ballot(have_base && act != bact);
                 keep_tiles = have_base && dif ? (__ffsll((long long)dif) - 1) / 5 : 0;
+                force_fact = false;
             }
 #endif
         }
@@ -663,81 +766,22 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
                 }
                 LMPC_SYNC();
             }
-            // K and its right-hand side on every lane (entries beyond nsch: identity); rows by their 3 entries
-            double Am[KM][KM], cv[KM], sg[KM];
-            int rb_[KM];
-            bool rw[KM];
+            // K's right-hand side c - V'y0 on every lane (entries beyond nsch: 0; the columns' V'y0 is in U already)
+            double cv[KM], sv[KM];
 #pragma unroll
             for (int i = 0; i < KM; ++i) {
                 const bool iv = i < nsch;
-                rw[i] = iv && utyp[iv ? i : 0] < 0.5;
-                rb_[i] = iv ? (int)uleg[i] : 0;
-                sg[i] = rw[i] ? -1.0 : 1.0;
-            }
-#pragma unroll
-            for (int i = 0; i < KM; ++i) {
-                const bool iv = i < nsch;
-                double a[3];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) a[q] = rw[i] ? U[4 * i + q] : 0.0;
+                const bool rwi = iv && utyp[iv ? i : 0] < 0.5;
+                const int rbi = iv ? (int)uleg[i] : 0;
                 double c = iv ? U[4 * i + 3] : 0.0;
-                if (rw[i]) {
+                if (rwi) {
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) c = fma(-a[q], S.lua[vidx(rb_[i], q)], c);
+                    for (int q = 0; q < 3; ++q) c = fma(-U[4 * i + q], S.lua[vidx(rbi, q)], c);
                 }
                 cv[i] = c;
-#pragma unroll
-                for (int j = 0; j <= i; ++j) {
-                    const bool jv = j < nsch;
-                    double v = (iv && jv) ? Cb[KM * i + j] : (i == j ? 1.0 : 0.0);
-                    if (iv && jv) {
-                        if (rw[i]) {
-#pragma unroll
-                            for (int q = 0; q < 3; ++q) v = fma(-a[q], Wc[64 * j + vidx(rb_[i], q)], v);
-                        } else if (rw[j]) {
-#pragma unroll
-                            for (int q = 0; q < 3; ++q) v = fma(-U[4 * j + q], Wc[64 * i + vidx(rb_[j], q)], v);
-                        }
-                    }
-                    Am[i][j] = v;
-                }
             }
-            // L D L' (lower triangle; D in dd)
-            bool bad = false;
-            double dd[KM];
-#pragma unroll
-            for (int c = 0; c < KM; ++c) {
-                double d = Am[c][c];
-#pragma unroll
-                for (int b = 0; b < c; ++b) d = fma(-Am[c][b], Am[c][b] * dd[b], d);
-                bad |= !(sg[c] * d > 1e-14 * fabs(Am[c][c]));
-                dd[c] = d;
-                const double inv = rcp_nr(d != 0.0 ? d : 1.0);
-#pragma unroll
-                for (int r = c + 1; r < KM; ++r) {
-                    double v = Am[r][c];
-#pragma unroll
-                    for (int b = 0; b < c; ++b) v = fma(-Am[r][b], Am[c][b] * dd[b], v);
-                    Am[r][c] = v * inv;
-                }
-            }
-            double sv[KM];
-#pragma unroll
-            for (int r = 0; r < KM; ++r) {  // L z = c
-                double v = cv[r];
-#pragma unroll
-                for (int b = 0; b < r; ++b) v = fma(-Am[r][b], sv[b], v);
-                sv[r] = v;
-            }
-#pragma unroll
-            for (int r = 0; r < KM; ++r) sv[r] = sv[r] * rcp_nr(dd[r] != 0.0 ? dd[r] : 1.0);
-#pragma unroll
-            for (int r = KM - 1; r >= 0; --r) {  // L' s = D^-1 z
-                double v = sv[r];
-#pragma unroll
-                for (int b = r + 1; b < KM; ++b) v = fma(-Am[b][r], sv[b], v);
-                sv[r] = v;
-            }
+            double kmin = 1.0;
+            const bool bad = schur_ksolve(cv, sv, kmin);
             double yv = S.lua[lane];
 #pragma unroll
             for (int j = 0; j < KM; ++j)
@@ -745,12 +789,20 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
             if (ncol && !bad && st) {
 #pragma unroll
                 for (int j = 0; j < KM; ++j) {
-                    if (j >= nsch || rw[j] || rb_[j] != lane) continue;
+                    if (j >= nsch || utyp[j] < 0.5 || (int)uleg[j] != lane) continue;
 #pragma unroll
                     for (int p = 0; p < 3; ++p) du[p] = fma(U[4 * j + p], sv[j], du[p]);
                 }
             }
-            // a rank-deficient update (rounding): keep y0; the round will not verify and the next one refactors
+#if LMPC_POLISH_REFINE
+            if (lane == 0) {  // s of this round, for the refinement of a verified round (polish verification below)
+#pragma unroll
+                for (int j = 0; j < KM; ++j) S.scr[DN_SCHUR_SV + j] = sv[j];
+                S.scr[DN_SCHUR_SV + KM] = kmin;
+            }
+#endif
+            // a rank-deficient update (rounding): keep y0; the round will not verify and the next one refactorises
+            // the same faces (a settled set that fails right after a range-space round, below)
             S.vec[lane] = bad ? S.lua[lane] : yv;
             if (bad) have_base = false;
             LMPC_SYNC();
@@ -923,10 +975,164 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
                 if (sr <= prm.tol_d * gscale)
 #endif
                 {
+#if LMPC_POLISH_SCHUR && LMPC_POLISH_REFINE
+                    if (schur && sr > LMPC_REFINE_SR * gscale) {
+                        // One step of iterative refinement of a verified range-space round.  The
+                        // update solves the round's bordered system [M V; V' Cb] [y; s] = [r0; c] through K = Cb - V'W,
+                        // W = M^-1 V; K's rounding, amplified by W, left config 2's forces up to ~2e-9 N from the optimum
+                        // (~1e-10 N refactorised).  The residuals come from the gradient G = H u + g in hand (S.vec2):
+                        //   base coordinates  rho_y = -T_b'G - (rows' a) lambda
+                        //   a column entry    rho_e = -t'G - (r't) lambda;   a row entry  rho_e = c_e - a'y - (r't) w
+                        // and the same factorisations give the correction: dy0 = M^-1 rho_y, K ds = rho_s - V'dy0,
+                        // dy = dy0 - W ds, du_b = T_b dy_b + t dw.  The refined forces are certified again (feasibility
+                        // of the free faces, stationarity / the apex cone test); if they fail, the verified ones stand.
+                        constexpr int KM = LMPC_SCHUR_KMAX;
+                        const ldouble* U = S.scr + 48;
+                        const ldouble* uleg = U + 4 * KM;
+                        const ldouble* utyp = uleg + KM;
+                        const ldouble* Cb = utyp + KM;
+                        const ldouble* Wc = S.scr + 128;
+                        const ldouble* Vc = Wc + 64 * nsch;
+                        const ldouble* svs = S.scr + DN_SCHUR_SV;
+                        double re = 0.0;  // entry residual (lane e)
+                        if (lane < nsch) {
+                            const int b = (int)uleg[lane];
+                            const bool row = utyp[lane] < 0.5;
+                            if (row) {
+                                re = U[4 * lane + 3];
+#pragma unroll
+                                for (int q = 0; q < 3; ++q) re = fma(-U[4 * lane + q], S.vec[vidx(b, q)], re);
+                            } else {
+#pragma unroll
+                                for (int p = 0; p < 3; ++p) re = fma(-U[4 * lane + p], S.vec2[vidx(b, p)], re);
+                            }
+#pragma unroll
+                            for (int f = 0; f < KM; ++f)
+                                if (f < nsch && (utyp[f] < 0.5) != row) re = fma(-Cb[KM * lane + f], svs[f], re);
+                        }
+                        // rho_y, lane = variable (16 t + 3 a + q <-> leg-step 5 t + a, component q)
+                        const int vw = lane & 15, vb = 5 * (lane >> 4) + vw / 3, vq = vw % 3;
+                        double ry = 0.0;
+                        if (vw < 15 && vb < nls) {
+                            const ldouble* Tb = S.blk + 9 * vb;
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) ry = fma(-Tb[3 * p + vq], S.vec2[vidx(vb, p)], ry);
+#pragma unroll
+                            for (int e = 0; e < KM; ++e)
+                                if (e < nsch && utyp[e] < 0.5 && (int)uleg[e] == vb) ry = fma(-U[4 * e + vq], svs[e], ry);
+                        }
+                        LMPC_SYNC();  // the reads of y above come first
+                        S.vec[lane] = ry;
+                        LMPC_SYNC();
+                        solve_vec();  // dy0 = M^-1 rho_y (the base factorisation, untouched by range-space rounds)
+                        const double dyl = S.vec[lane];
+                        double rc = re;
+                        if (lane < nsch && utyp[lane] < 0.5) {
+                            const int b = (int)uleg[lane];
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) rc = fma(-U[4 * lane + q], S.vec[vidx(b, q)], rc);
+                        }
+                        double cv[KM], dsv[KM];
+#pragma unroll
+                        for (int e = 0; e < KM; ++e) {
+                            cv[e] = 0.0;
+                            if (e < nsch) {  // wave-uniform
+                                double c = readlane_f64(rc, e);
+                                const double ty = utyp[e];
+                                if (ty > 0.5) c -= wave_sum(Vc[64 * ((int)ty - 1) + lane] * dyl);
+                                cv[e] = c;
+                            }
+                        }
+                        double kmin2 = 1.0;
+                        const bool bad2 = schur_ksolve(cv, dsv, kmin2);
+                        double dy = dyl;
+#pragma unroll
+                        for (int j = 0; j < KM; ++j)
+                            if (j < nsch) dy = fma(-Wc[64 * j + lane], dsv[j], dy);
+                        LMPC_SYNC();
+                        S.vec[lane] = dy;
+                        LMPC_SYNC();
+                        double ur[3] = {u[0], u[1], u[2]};
+                        if (st && !apex) {
+                            const ldouble* Tb = S.blk + 9 * lane;
+                            double d3[3];
+#pragma unroll
+                            for (int a = 0; a < 3; ++a) d3[a] = S.vec[vidx(lane, a)];
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) ur[p] += Tb[3 * p] * d3[0] + Tb[3 * p + 1] * d3[1] + Tb[3 * p + 2] * d3[2];
+#pragma unroll
+                            for (int j = 0; j < KM; ++j) {
+                                if (j >= nsch || utyp[j] < 0.5 || (int)uleg[j] != lane) continue;
+#pragma unroll
+                                for (int p = 0; p < 3; ++p) ur[p] = fma(U[4 * j + p], dsv[j], ur[p]);
+                            }
+                        }
+                        // certify the refined forces
+                        S.vec2[lane] = 0.0;
+                        LMPC_SYNC();
+                        if (st) {
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) S.vec2[vidx(lane, p)] = ur[p];
+                        }
+                        LMPC_SYNC();
+                        const double gr = h_matvec(S, S.vec2, S.scr, lane) + S.gv[lane];
+                        LMPC_SYNC();
+                        S.vec2[lane] = gr;
+                        LMPC_SYNC();
+                        double g2[3] = {0.0, 0.0, 0.0}, gl2 = 1.0;
+                        if (st) {
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) {
+                                g2[p] = S.vec2[vidx(lane, p)];
+                                gl2 = fmax(gl2, fabs(g2[p]));
+                            }
+                        }
+                        const double gs2 = wave_max(gl2);
+                        bool ok = !bad2;
+                        if (st) {
+                            double o[5];
+                            cons_resid(ur, mu, fzmax, o);
+#pragma unroll
+                            for (int i = 0; i < 5; ++i)
+                                if (!((act >> i) & 1) && o[i] > prm.tol_p * fzmax) ok = false;
+                            if (apex) {
+                                ok = ok && !(g2[2] / mu < fabs(g2[0]) + fabs(g2[1]) - prm.tol_d * gs2);
+                            } else {
+                                const LegKkt kk = leg_kkt(act, g2, mu, -prm.tol_d * gs2);
+                                ok = ok && kk.drop < 0 && kk.res <= prm.tol_d * gs2;
+                            }
+                        }
+#ifdef LMPC_REFINE_DIAG
+                        {
+                            double dl = 0.0;
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) dl = fmax(dl, fabs(ur[p] - u[p]));
+                            dl = wave_max(dl);
+                            const bool allok = __all(ok);
+                            if (lane == 0 && qp < LMPC_KKT_DIAG_QPS) {
+                                lmpc_refine_diag[qp][0] = sr / gscale;
+                                lmpc_refine_diag[qp][1] = S.scr[DN_SCHUR_SV + KM];
+                                lmpc_refine_diag[qp][2] = dl;
+                                lmpc_refine_diag[qp][3] = allok ? 1.0 : 2.0;
+                            }
+                        }
+#endif
+                        if (__all(ok)) {
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) u[p] = ur[p];
+                        }
+                    }
+#endif
                     done = true;
                     break;
                 }
-                rd = prm.max_rounds - 1;
+#if LMPC_POLISH_SCHUR
+                if (schur && !refact_done) {
+                    force_fact = true;  //  the same faces once more, factorised, before the retry ladder
+                    refact_done = true;
+                } else
+#endif
+                    rd = prm.max_rounds - 1;
             }
             keep_tiles = chg ? (__ffsll((long long)chg) - 1) / 5 : 0;  // tile of the first changed leg-step
             if (++rd >= prm.max_rounds) {

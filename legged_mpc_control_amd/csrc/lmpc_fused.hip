@@ -15,7 +15,7 @@
 // The product build only: the diagnostic and test-variant builds (stamps, certificate residuals, re-injected bugs,
 // debug dumps) keep the two launches, so their hooks and their bugs stay in one translation unit each
 #if !defined(LMPC_STAMPS) && !defined(LMPC_KKT_DIAG) && !defined(LMPC_BUG_ZA) && !defined(LMPC_BUG_YAW) && \
-    !defined(LMPC_KKT_OFF) && !defined(LMPC_LQ_DEBUG) && !defined(LMPC_NO_FUSED)
+    !defined(LMPC_KKT_OFF) && !defined(LMPC_LQ_DEBUG) && !defined(LMPC_NO_FUSED) && !defined(LMPC_REFINE_DIAG)
 #define LMPC_FUSED 1
 #include "lmpc_dense_kernel.h"
 #include "lmpc_lq_kernel.h"

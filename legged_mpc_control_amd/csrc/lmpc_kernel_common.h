@@ -34,8 +34,8 @@ constexpr int LMPC_WAVE = 64;
 #ifndef LMPC_ACT_RATIO
 #define LMPC_ACT_RATIO 1e-3
 #endif
-// diagnostic builds only (-DLMPC_KKT_DIAG): per-QP certificate residuals kept for this many QPs per kernel
-#ifdef LMPC_KKT_DIAG
+// diagnostic builds only (-DLMPC_KKT_DIAG, -DLMPC_REFINE_DIAG): per-QP certificate residuals kept for this many QPs
+#if defined(LMPC_KKT_DIAG) || defined(LMPC_REFINE_DIAG)
 #define LMPC_KKT_DIAG_QPS 65536
 #endif
 #define LMPC_SYNC()                                              \

@@ -144,3 +144,28 @@ def test_certificate_passes_every_golden_qp(dense):
         g, st, _ = s.solve(d["rec"], d["contact"], normals=d["normals"])
         assert (st == 0).all(), (os.path.basename(path), st)
         assert rel_err(g, d["grf"]) <= 1e-7, os.path.basename(path)
+
+
+@pytest.mark.gpu
+def test_range_space_rounds_match_refactorised_rounds():
+    """the dense polish's range-space rounds (rows-only and bordered updates of the last factorisation,
+    lmpc_dense_kernel.h) against a build that refactorises every round (LMPC_POLISH_SCHUR=0): the same iteration words
+    and status on a config-2 batch, forces within rounding of each other and of the oracle -- and not bit-identical
+    (so the updates really ran).  The batch is the bench's first 1024 QPs, which holds the QP whose update ended
+    1.8e-9 from the optimum in round 5; the refinement of such rounds (LMPC_POLISH_REFINE) brings it back to <= 2e-10."""
+    from legged_mpc_control_amd import _native as N
+    from legged_mpc_control_amd import synth
+    from oracle import oracle as O
+
+    p, H, rec, con = synth.config_batch(2, count=1024, first_index=0)
+    ref, _, _ = O.solve_batch(O.params_from(p), H, rec, con, n_threads=8)
+    g0, st0, it0 = _solve_with(N.lib(), p, H, rec, con, dense=1)
+    g1, st1, it1 = _solve_with(_variant("noschur"), p, H, rec, con, dense=1)
+    assert (st0 == 0).all() and (st1 == 0).all()
+    assert (it0 == it1).all(), f"iteration words differ on {(it0 != it1).sum()} QPs"
+    e0, e1 = _per_qp_err(g0, ref), _per_qp_err(g1, ref)
+    print(f"range-space updates: max err {e0.max():.3g}; refactorised: {e1.max():.3g}; "
+          f"QPs whose bits differ: {(g0 != g1).any(axis=(1, 2)).sum()}")
+    assert e0.max() <= 2e-10 and e1.max() <= 2e-10
+    assert np.max(np.abs(g0 - g1)) <= 1e-9
+    assert (g0 != g1).any(axis=(1, 2)).sum() > 0, "no range-space round ran: the test proves nothing"
