@@ -22,35 +22,37 @@ HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
 
 
 # ---- the LDS Riccati kernel (lmpc_lq.hip, round 4 on): useful flops of the formulation it runs -----------------
-#   Counted from the algorithm on the nonzero structure (FMA = 2 flops), not from the padded
-# 16x16 MFMA tiles or the exec-masked lanes the PMC counters see; n = 12 states, 13 with the affine column of P^,
-# m = 6 rows reached by the inputs (6-11), dt N(yaw) has 8 nonzeros.  Per horizon stage:
-#   interior-point factorisation (reduced inputs, six unit-cost inputs f = U v - g):
-#     U = chol(W) 36 + C = P^[:,6:12] [U | dv] 13 x 27 = 351 + Guu' = I + U'(P22 U) 91 + chol(Guu') 36
-#     + X = L^-1 U' 90 + K = X'X 126 + P^ dtN 104 + KZ = K Z 468 + dtN' PA 104 + PA' KZ (symmetric) 546 = 1952 FMA
+# (pinned in round 6)  Counted on the nonzero structure of the operands, not
+# on the padded 16x16 MFMA tiles or the exec-masked lanes the PMC counters see: tests/test_flop_models.py restates
+# every operation below in numpy on matrices with the kernel's structure (checked for what they compute: the Riccati
+# step against the direct formula, W_j against Bt Rr^-1 Bt') and counts each product as executed (FMA = 2 flops, a
+# lone multiply, division, sqrt or reciprocal 1); the constants are those counts in FMA units (flops / 2).  Round 5's
+# hand tallies were 4 % (factorisations) to 2x (leg-step terms, which multiplied G0_j's structural zeros) higher, in
+# all 13-15 % over the count.  Per horizon stage:
+#   interior-point factorisation (reduced inputs, six unit-cost inputs f = U v - g): U = chol(W), C = P^[:,6:12]
+#     [U | dv], Guu' = I + U'(P22 U), chol(Guu'), X = L^-1 U', K = X'X, P^ dtN, KZ = K Z, dtN' PA, PA' KZ (symmetric)
 #   polish factorisation: the same in reduced inputs where W_k is well conditioned (one leg-step per lane), plus the
-#     linear term's column (13 x 6 + 6 x 6 = 114); full inputs (two leg-steps per lane: H > 16):
-#     C = P^[:,6:12] [Bt | dv] 13 x 6 x 13 = 1014 + Guu = Rr + Bt'P22 Bt 78 x 6 = 468 + block Cholesky, L^-1 and
-#     X = L^-1 [Bt' | r] 288 + 504 + KH = X'X (7 x 7) 336 + PA 104 + KZ 468 + P 650 = 3832 FMA
-#   per Newton system: forward sweep 6 x 12 + 8 = 80, costate lambda2 = Z A^-1 x' 80                  = 160 FMA
-#   corrector: P22 dg 72 + rho 36 + q' 72 + backward sweep 80 + t = K za + rho 36                     = 296 FMA
-#   polish verification: B u rows 36, dynamics rows 36, tracking 12, adjoint 20                      =  104 FMA
+#     linear term's column; full inputs (two leg-steps per lane: H > 16): C = P^[:,6:12] [Bt | dv], Guu = Rr +
+#     Bt'P22 Bt, its Cholesky with X = L^-1 [Bt' | rr] alongside, KH = X'X, PA, KZ, P
+#   per Newton system: forward sweep x' = A x + dv - KZ x - t, costate lambda2 = Z A^-1 x'
+#   corrector: P22 dg, rho, q' = q - Z'rho, the backward sweep, t = K za + rho
+#   polish verification: B u rows, dynamics rows, tracking terms, adjoint step
 # per stance leg-step:
-#   interior point, per factorisation: W, C'WC, Rr and its Cholesky, L^-1 rr, Y = G0_j L^-T, g_j, W_j = Y Y'  150 FMA
-#   polish, per factorisation: null basis, T'RbT, rr, Bt = G0 T, Y and W_j                                   260 FMA
-#   per Newton system: G0_j' lambda2, the 3 x 3 solve, the step-length terms                                  60 FMA
-#   polish verification: G0_j u, g = R u + G0_j' lambda, the multiplier fit and the stationarity residual   100 FMA
-# per stage and factorisation: the quad sums of W_j and g_j (27 entries x 3 adds)                             81 flops
-LQ_IPM_FACT_FMA = 1952
-LQ_POL_FACT_RED_FMA = 1952 + 114
-LQ_POL_FACT_FULL_FMA = 3832
+#   interior point, per factorisation: W = z/s, C'WC, Rr and its Cholesky, L^-1 rr, Y = G0_j L^-T, g_j, W_j = Y Y'
+#   polish, per factorisation (one active face, the common case): null basis, T'RbT, rr, Bt = G0 T, G0 up, Y, W_j
+#   per Newton system: G0_j' lambda2, the 3 x 3 solve, the step-length terms
+#   polish verification: G0_j u, g = R u + G0_j' lambda, the multiplier fit and the stationarity residual
+# per stage and factorisation: the quad sums of W_j and g_j (27 entries x 3 adds)
+LQ_IPM_FACT_FMA = 1876
+LQ_POL_FACT_RED_FMA = 1980.5
+LQ_POL_FACT_FULL_FMA = 3326
 LQ_SYSTEM_FMA = 160
-LQ_CORR_FMA = 296
-LQ_VERIFY_FMA = 104
-LQ_LEG_IPM_FMA = 150
-LQ_LEG_POL_FMA = 260
-LQ_LEG_SYSTEM_FMA = 60
-LQ_LEG_VERIFY_FMA = 100
+LQ_CORR_FMA = 298
+LQ_VERIFY_FMA = 49
+LQ_LEG_IPM_FMA = 89
+LQ_LEG_POL_FMA = 117
+LQ_LEG_SYSTEM_FMA = 42
+LQ_LEG_VERIFY_FMA = 48.5
 LQ_QUAD_FLOP = 81
 
 
