@@ -32,6 +32,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup-ms", type=float, default=30.0,
+                    help="keep warming up (after --warmup steps) until the device has run this long (clock ramp)")
     ap.add_argument("--config", type=int, default=2, help="BASELINE.json config id (2,3,4,5)")
     ap.add_argument("--batch", type=int, default=None, help="QPs per GPU (default: config batch; config 4: 65536/N)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall seconds)")
@@ -156,25 +158,37 @@ def main():
     stream = torch.cuda.Stream(dev)  # dedicated launch stream: events below bracket exactly the kernels
     torch.cuda.set_stream(stream)
 
-    for _ in range(args.warmup):
-        solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream, normals=d_nrm)
-    torch.cuda.synchronize(dev)
+    # Warm-up: the W steps asked for, then more until the device has been busy for --warmup-ms: the GPU's clocks ramp
+    # up over the first ~10-20 ms of sustained load, and a timed region that starts on a cold GPU measures the ramp
+    # (config 2 at --warmup 5: 0.171 ms per step, the launches themselves 0.170; after 50 warm-up steps 0.165 / 0.164,
+    # tools/r6_steps.sh, profiles/r06/steps/).  The line reports both counts.
+    warm_run = 0
+    tw = time.perf_counter()
+    while warm_run < args.warmup or time.perf_counter() - tw < args.warmup_ms * 1e-3:
+        for _ in range(args.warmup if warm_run == 0 and args.warmup > 0 else 4):
+            solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream, normals=d_nrm)
+            warm_run += 1
+        torch.cuda.synchronize(dev)
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # One HIP event pair on the launch stream brackets the K launches of the timed region: kernel_ms = its elapsed
+    # time / K, the average launch duration (back-to-back launches leave no measurable gap between them).  Until
+    # round 5 every step had its own event pair, and those events cost ~5 us per step of their own: config 2 ran
+    # 0.176 ms per step with them against 0.167 without (tools/step_overhead.py, profiles/r06/overhead/).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        evs[i][0].record(stream)
         solver.solve_device(d_rec, d_con, d_grf, d_st, d_it, stream, normals=d_nrm)
-        evs[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     t_max = D.max_over_ranks(elapsed, dist, dev)
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     # N > 1: a second timed pass, solve + grouped point-to-point gather of every rank's GRFs to
     # rank 0 (SURVEY.md 8e "with and without the gather"); reported beside `value`, never as it.
@@ -363,6 +377,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warm_run,
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",

@@ -29,6 +29,11 @@
  * factor workspace, hand-over flags and staging blocks are shared by every
  * entry point): an asynchronous device-path call on stream A followed by a
  * call on stream B or a host-pointer call makes B / the host wait for A.
+ * The wait is set up when the stream changes (an event recorded on A at the
+ * call on B), so back-to-back calls on one stream pay no event at all; stream
+ * A must therefore still exist at the context's next device-path call on
+ * another stream (a host-pointer call, lmpc_sync and lmpc_destroy wait for the
+ * device instead and have no such requirement).
  *
  * Per-instance record layout (doubles, see lmpc_record_len):
  *   [ x0(12) | rot(9, row-major body->world) | feet(4 legs x xyz, world-aligned,

@@ -58,11 +58,16 @@ struct lmpc_ctx {
     uint8_t* d_ccon = nullptr;
     size_t cmd_qps = 0;
     // Ordering of the context's own buffers (d_scratch, d_done, the staging blocks, d_crec/d_ccon) across
-    // streams: recorded after every launch that uses them, waited on by the next such launch when it comes on
-    // another stream (ctx_enter / ctx_leave).
+    // streams: a launch that uses them notes its stream (ctx_leave); the next such launch on another stream
+    // records `ev` on the noted stream then and waits on it (ctx_enter); a host-pointer call, lmpc_sync and
+    // lmpc_destroy wait for the device instead (the noted stream may be gone by then).  Calls on one stream pay
+    // no event: recording one after every launch cost config 2 ~3 us per step (1.8 %, round 6,
+    // profiles/r06/overhead/).
     hipEvent_t ev = nullptr;
-    hipStream_t ev_stream = nullptr;
+    hipStream_t ev_stream = nullptr;  // where ev was last recorded
     bool ev_live = false;
+    hipStream_t last = nullptr;       // stream of the last launch that used the buffers, not yet fenced
+    bool pend = false;
 };
 
 namespace {
@@ -136,18 +141,38 @@ bool stream_ok(hipStream_t s, int dev) {
     return hipStreamGetDevice(s, &d) == hipSuccess && d == dev;
 }
 
-// Launches that use the context's buffers are ordered as issued, whatever stream each comes on: before one,
-// the stream waits for the event recorded after the previous one (when that ran on another stream); after
-// it, the event is recorded again.  Device-path calls on a single stream pay one event record each.
+// Launches that use the context's buffers are ordered as issued, whatever stream each comes on.  ctx_leave notes
+// the launch's stream; ctx_enter, before a launch on stream s, records the event on a noted launch's stream when s
+// differs (everything issued there so far precedes it) and makes s wait for it.  A launch on the noted stream needs
+// nothing: stream order already holds.
 hipError_t ctx_enter(lmpc_ctx* c, hipStream_t s) {
+    if (c->pend) {
+        if (c->last == s) return hipSuccess;
+        const hipError_t e = hipEventRecord(c->ev, c->last);
+        c->pend = false;
+        c->ev_stream = c->last;
+        c->ev_live = e == hipSuccess;
+        if (e != hipSuccess) return e;
+    }
     if (c->ev_live && c->ev_stream != s) return hipStreamWaitEvent(s, c->ev, 0);
     return hipSuccess;
 }
 hipError_t ctx_leave(lmpc_ctx* c, hipStream_t s) {
-    const hipError_t e = hipEventRecord(c->ev, s);
-    c->ev_stream = s;
-    c->ev_live = e == hipSuccess;
-    return e;
+    c->last = s;
+    c->pend = true;
+    return hipSuccess;
+}
+// Wait on the host for the last launch that used the context's buffers (its stream may have been destroyed since:
+// the device as a whole, which is rare -- a host-pointer call after device-path calls on another stream, lmpc_sync,
+// lmpc_destroy).
+hipError_t ctx_wait_host(lmpc_ctx* c, hipStream_t s) {
+    if (c->pend && c->last != s) {
+        const hipError_t e = hipDeviceSynchronize();
+        c->pend = false;
+        return e;
+    }
+    if (c->ev_live && c->ev_stream != s) return hipEventSynchronize(c->ev);
+    return hipSuccess;
 }
 
 void free_bufs(lmpc_ctx* c) {
@@ -282,7 +307,7 @@ void lmpc_destroy(lmpc_ctx* c) {
     if (!c) return;
     DeviceScope ds(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->ev_live) (void)hipEventSynchronize(c->ev);  // the last launch on a caller's stream
+    (void)ctx_wait_host(c, c->stream);  // the last launch on a caller's stream
     free_bufs(c);
     if (c->ev) (void)hipEventDestroy(c->ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -400,7 +425,7 @@ static int solve_host(lmpc_ctx* c, const double* rec, const uint8_t* contact, co
     const size_t nact = act_in ? ncon : 0;
     // the pinned staging blocks and the factor scratch may still be in use by an earlier asynchronous
     // device-path call on another stream: wait for it before the host writes the staging block
-    if (c->ev_live && c->ev_stream != s && hipEventSynchronize(c->ev) != hipSuccess) return LMPC_ERR_DEVICE;
+    if (ctx_wait_host(c, s) != hipSuccess) return LMPC_ERR_DEVICE;
     std::memcpy(c->h_in, rec, nrec);
     if (normals) std::memcpy(c->h_in + nrec, normals, nnrm);
     std::memcpy(c->h_in + nrec + nnrm, contact, ncon);
@@ -568,7 +593,7 @@ int lmpc_sync(lmpc_ctx* c) {
     if (!ds.ok) return LMPC_ERR_DEVICE;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return LMPC_ERR_DEVICE;
     // and the last launch that used the context's buffers, whatever stream it ran on
-    return !c->ev_live || hipEventSynchronize(c->ev) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
+    return ctx_wait_host(c, c->stream) == hipSuccess ? LMPC_OK : LMPC_ERR_DEVICE;
 }
 
 }  // extern "C"
