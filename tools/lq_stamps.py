@@ -36,6 +36,25 @@ for i, nm in enumerate(names):
     c = calls[i].mean()
     print(f"  {nm:14s} {m:11.0f} ({100 * m / tot.mean():5.1f}%)  per call {m / max(c, 1e-9):8.0f}  per stage {m / max(c, 1e-9) / H:6.0f}")
 
+# Dispatch tail (round 6): the launch's QPs run on `slots` wave slots (4 per CU at H > 16 and at H <= 16 with one
+# wave per SIMD, 8 at two waves per SIMD), each slot taking the next QP when it frees -- list scheduling in index
+# order, which is what the dispatcher does.  Against the mean load per slot and against longest-first order.
+import heapq  # noqa: E402
+
+
+def makespan(costs, m):
+    h = [0.0] * m
+    for c in costs:
+        heapq.heappush(h, heapq.heappop(h) + c)
+    return max(h)
+
+
+slots = 256 * (8 if (4 * H <= 64 and count > 1024) else 4)
+if count > slots:
+    ms_list, ms_lpt, mean_load = makespan(tot, slots), makespan(np.sort(tot)[::-1], slots), tot.sum() / slots
+    print(f"dispatch tail on {slots} slots: mean load {mean_load:.0f} cycles, index order {ms_list:.0f} "
+          f"({ms_list / mean_load:.3f}x), longest first {ms_lpt:.0f} ({ms_lpt / mean_load:.3f}x)")
+
 s2 = BatchedConvexQPSolver(p, H, max_batch=count, dense_path="off", riccati_path="scratch")
 grf2, st2, it2 = s2.solve(rec, con)
 L.lmpc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
