@@ -28,9 +28,14 @@ struct lmpc_hoqp_ctx {
     size_t scratch_inst = 0;
     double* d_z = nullptr;      // host path staging: stacked Z matrices + column counts (allocated on first use)
     int32_t* d_zc = nullptr;
-    hipEvent_t ev = nullptr;    // orders launches that share d_scratch across streams
+    // orders launches that share d_scratch across streams: recorded on the last launch's stream only when the next
+    // one comes on another stream (as lmpc_capi.cpp, round 6: back-to-back launches on one stream pay no event);
+    // host-side waits (scratch growth, lmpc_hoqp_sync, lmpc_hoqp_destroy) wait for the device instead
+    hipEvent_t ev = nullptr;
     hipStream_t ev_stream = nullptr;
     bool ev_live = false;
+    hipStream_t last = nullptr;
+    bool pend = false;
 };
 
 namespace {
@@ -108,7 +113,9 @@ hipError_t ensure_scratch(lmpc_hoqp_ctx* c, int batch) {
     if (e != hipSuccess) return e;
     if (c->d_scratch) {
         // an earlier launch on another stream may still use the old block
-        if (c->ev_live) (void)hipEventSynchronize(c->ev);
+        if (c->pend) (void)hipDeviceSynchronize();
+        else if (c->ev_live) (void)hipEventSynchronize(c->ev);
+        c->pend = false;
         (void)hipFree(c->d_scratch);
     }
     c->d_scratch = p;
@@ -126,12 +133,19 @@ hipError_t launch(lmpc_hoqp_ctx* c, const double* rec, int batch, double* x, dou
                   double* z, int32_t* zc, hipStream_t s) {
     hipError_t e = ensure_scratch(c, batch);
     if (e != hipSuccess) return e;
-    if (c->ev_live && c->ev_stream != s && (e = hipStreamWaitEvent(s, c->ev, 0)) != hipSuccess) return e;
+    if (c->pend && c->last != s) {
+        e = hipEventRecord(c->ev, c->last);
+        c->pend = false;
+        c->ev_stream = c->last;
+        c->ev_live = e == hipSuccess;
+        if (e != hipSuccess) return e;
+    }
+    if (!(c->pend && c->last == s) && c->ev_live && c->ev_stream != s && (e = hipStreamWaitEvent(s, c->ev, 0)) != hipSuccess)
+        return e;
     e = lmpc::launch_hoqp(c->P, rec, batch, x, w, st, it, z, zc, c->d_scratch, s);
     if (e != hipSuccess) return e;
-    e = hipEventRecord(c->ev, s);
-    c->ev_stream = s;
-    c->ev_live = e == hipSuccess;
+    c->last = s;
+    c->pend = true;
     return e;
 }
 
@@ -213,7 +227,8 @@ void lmpc_hoqp_destroy(lmpc_hoqp_ctx* c) {
     if (!c) return;
     DeviceScope scope(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->ev_live) (void)hipEventSynchronize(c->ev);
+    if (c->pend && c->last != c->stream) (void)hipDeviceSynchronize();  // its stream may be gone by now
+    else if (c->ev_live) (void)hipEventSynchronize(c->ev);
     (void)hipFree(c->d_rec);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_st);
@@ -258,6 +273,12 @@ int lmpc_hoqp_solve_batch_z(lmpc_hoqp_ctx* c, const double* tasks, int batch, do
     int32_t* d_status = c->d_st;
     int32_t* d_iters = c->d_st + batch;
     hipStream_t s = c->stream;
+    // a device-path launch still pending on a caller's stream: wait for the device (that stream may be gone)
+    if (c->pend && c->last != s) {
+        if (hipDeviceSynchronize() != hipSuccess) return LMPC_ERR_DEVICE;
+        c->pend = false;
+        c->ev_live = false;
+    }
     if (hipMemcpyAsync(c->d_rec, tasks, (size_t)batch * c->P.rec_len * sizeof(double), hipMemcpyHostToDevice, s) !=
         hipSuccess)
         return LMPC_ERR_DEVICE;
@@ -309,7 +330,8 @@ int lmpc_hoqp_sync(lmpc_hoqp_ctx* c) {
     DeviceScope scope(c->device);
     if (!scope.ok) return LMPC_ERR_DEVICE;
     bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
-    if (c->ev_live) ok = ok && hipEventSynchronize(c->ev) == hipSuccess;
+    if (c->pend && c->last != c->stream) ok = ok && hipDeviceSynchronize() == hipSuccess;
+    else if (c->ev_live) ok = ok && hipEventSynchronize(c->ev) == hipSuccess;
     return ok ? LMPC_OK : LMPC_ERR_DEVICE;
 }
 
