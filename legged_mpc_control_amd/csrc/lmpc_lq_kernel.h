@@ -124,6 +124,10 @@ __device__ __forceinline__ double lq_Ax(Ptr x, int r, double ck, double sk, doub
 #ifndef LMPC_LQ_HOIST
 #define LMPC_LQ_HOIST 3
 #endif
+// the same choice for the two-wave instance at two leg-steps per lane (round 6: H = 17..26)
+#ifndef LMPC_LQ_HOIST_LS2W2
+#define LMPC_LQ_HOIST_LS2W2 3
+#endif
 // At two waves per SIMD the reduced stage reads its U row after the pivot staging and stores Z_k after the solve
 // (shorter live ranges across the 6 x 6 factor; the lone-wave instances keep the early read, 2 % faster there -- the
 // same arithmetic either way, so every instance gives the same bits); 0 = the early read everywhere (diagnostic)
@@ -253,6 +257,7 @@ __device__ __forceinline__ void lq_body(const DevParams prm, const double* __res
     // default since round 5); at two waves per SIMD the second set of registers would spill
     constexpr bool LQ_PF = LMPC_LQ_PF && WPE == 1;
     constexpr bool LQ_LATE = LQ_LATE_ON && WPE == 2;
+    constexpr int LQ_HOIST = (LS == 2 && WPE == 2) ? LMPC_LQ_HOIST_LS2W2 : LMPC_LQ_HOIST;
     // reduced-input polish stages (well-conditioned W_k) at one leg-step per lane: measured -1.2 % on config 4 (stages
     // with three or four stance legs), +2.5 % on config 2 with the dense path off (a trot's full polish stage has only
     // two pivot blocks); both instances alike, as kzs above; at two leg-steps per lane the leg-step work is not repaid
@@ -807,7 +812,7 @@ __device__ __forceinline__ void lq_body(const DevParams prm, const double* __res
                     double bg[2], xg[3], qn[3], ckn, skn;
                     bool sfn;
                     auto fetch = [&](int k) {
-                        const int fl = (LMPC_LQ_HOIST & 2) ? sfl : lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
+                        const int fl = (LQ_HOIST & 2) ? sfl : lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                         const ldouble* sl = slots + k * LQ_SLOT;
                         ckn = cs[2 * k];
                         skn = cs[2 * k + 1];
@@ -848,7 +853,7 @@ __device__ __forceinline__ void lq_body(const DevParams prm, const double* __res
                     };
                     fetch(H - 1);
                     for (int k = H - 1; k >= 0; --k) {
-                        const int fl = (LMPC_LQ_HOIST & 1) ? sfl : lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
+                        const int fl = (LQ_HOIST & 1) ? sfl : lq_lane<WPE>(lane), lc = fl & 15, lr = fl >> 4;
                         ldouble* sl = slots + k * LQ_SLOT;
                         const double ck = ckn, sk = skn;
                         const bool sr = red || sfn;
