@@ -1,4 +1,4 @@
-"""world_size-2 gloo test of the multi-rank path (CPU): every rank builds its own
+"""world_size-2 and -4 gloo tests of the multi-rank path (CPU): every rank builds its own
 shard from (seed, global index), solves it (here with the oracle standing in for
 the device solve), and rank 0 gathers the GRFs point-to-point; the gathered
 batch must equal a single-process solve of the global batch, and the bench
@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 
@@ -49,8 +50,8 @@ def _worker(rank, world, port, out_dir, per_rank):
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_gather(tmp_path):
-    world, per_rank = 2, 6
+@pytest.mark.parametrize("world,per_rank", [(2, 6), (4, 3)])
+def test_multi_rank_shard_and_gather(tmp_path, world, per_rank):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), per_rank), nprocs=world, join=True)
     from legged_mpc_control_amd import synth
     from oracle import oracle as O
@@ -61,7 +62,7 @@ def test_two_rank_shard_and_gather(tmp_path):
     assert gathered.shape == ref.shape
     assert np.array_equal(gathered, ref)
     t, ok, nfail = np.load(tmp_path / "reduced.npy")
-    assert t == 2.0 and ok == world * per_rank - 1 and nfail == 0
+    assert t == float(world) and ok == world * per_rank - 1 and nfail == 0
 
 
 def test_split_range_covers_total():
