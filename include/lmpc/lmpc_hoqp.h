@@ -95,7 +95,9 @@ int lmpc_hoqp_set_options(lmpc_hoqp_ctx* ctx, const lmpc_hoqp_options* o);
 int lmpc_hoqp_solve_batch(lmpc_hoqp_ctx* ctx, const double* tasks, int batch, double* x, double* slack,
                           int32_t* status, int32_t* iters);
 /* Device buffers (resident in HBM), asynchronous on `stream` (hipStream_t; NULL = the null stream, as in
- * lmpc.h).  status / iters may be NULL. */
+ * lmpc.h).  status / iters may be NULL.  Calls on one context are ordered as issued across streams, as in lmpc.h:
+ * the event is recorded on the last call's stream when the next device-path call comes on another one, so that
+ * stream must still exist then (host-pointer calls, lmpc_hoqp_sync and lmpc_hoqp_destroy wait for the device). */
 int lmpc_hoqp_solve_device(lmpc_hoqp_ctx* ctx, const double* d_tasks, int batch, double* d_x, double* d_slack,
                            int32_t* d_status, int32_t* d_iters, void* stream);
 int lmpc_hoqp_sync(lmpc_hoqp_ctx* ctx);
