@@ -287,6 +287,11 @@ class BatchedConvexQPSolver:
                 "lmpc_grf_to_torque_device")
         return tau
 
+    def sync(self) -> None:
+        """Wait for everything the context has issued (lmpc_sync): its own stream and its last device-path launch on
+        a caller's stream."""
+        N.check(self._L.lmpc_sync(self._ctx), "lmpc_sync")
+
     def close(self) -> None:
         if self._ctx:
             self._L.lmpc_destroy(self._ctx)

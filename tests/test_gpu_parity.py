@@ -614,6 +614,44 @@ def test_mixed_streams_and_host_path_share_one_context(torch_dev):
     assert np.array_equal(o3.cpu().numpy(), ref3)
 
 
+def test_stream_gone_before_the_next_call(torch_dev):
+    """Round 6: a context records its cross-stream ordering event only when the stream changes, so a device-path call
+    on a caller's stream A leaves nothing recorded on A.  If A is destroyed right after that call (its solve still
+    running), the context's next host-pointer call, lmpc_sync and lmpc_destroy must wait for the device instead of
+    touching A: no crash, and every result equals the same solve run alone."""
+    import ctypes
+
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    p, H, rec, con = synth.config_batch(3, count=4096, first_index=7)     # H = 20: milliseconds of Riccati kernel
+    _, _, rec2, con2 = synth.config_batch(3, count=512, first_index=70001)
+    s = BatchedConvexQPSolver(p, H, max_batch=512)
+    d_rec, d_con = torch.from_numpy(rec).to(torch_dev), torch.from_numpy(con).to(torch_dev)
+    ref1 = torch.empty((rec.shape[0], H, 12), dtype=torch.float64, device=torch_dev)
+    s.solve_device(d_rec, d_con, ref1)
+    torch.cuda.synchronize()
+    ref2, _, _ = s.solve(rec2, con2)
+    for after in ("host", "sync", "destroy"):
+        t = BatchedConvexQPSolver(p, H, max_batch=512)
+        a = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(a), 1) == 0  # hipStreamNonBlocking
+        out = torch.empty_like(ref1)
+        torch.cuda.synchronize()
+        t.solve_device(d_rec, d_con, out, stream=a.value)   # returns at once
+        assert hip.hipStreamDestroy(a) == 0                 # the caller's stream is gone; its solve may still run
+        if after == "host":
+            g2, st2, _ = t.solve(rec2, con2)               # host path: waits for the device, never for A
+            assert np.array_equal(g2, ref2) and np.all(st2 == 0)
+        elif after == "sync":
+            t.sync()
+        t.close()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref1), after
+
+
 def test_python_dropin_warm_ticks_match_oracle():
     """The Python drop-in warm-starts by default, like the C++ one: over consecutive ticks of a trot (FSM phase
     advancing, state drifting) every tick's u_0 equals the oracle's, and the later ticks re-verify the shifted
