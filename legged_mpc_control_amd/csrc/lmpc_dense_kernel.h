@@ -48,6 +48,25 @@
 #ifndef LMPC_POLISH_BORDER
 #define LMPC_POLISH_BORDER 1
 #endif
+// Gondzio centrality correctors per interior-point iteration (0: none, the product; diagnostic A/B)
+#ifndef LMPC_GONDZIO
+#define LMPC_GONDZIO 0
+#endif
+#ifndef LMPC_GZ_SKIP
+#define LMPC_GZ_SKIP 0.9
+#endif
+#ifndef LMPC_GZ_DA
+#define LMPC_GZ_DA 0.2
+#endif
+#ifndef LMPC_GZ_GAMMA
+#define LMPC_GZ_GAMMA 0.1
+#endif
+#ifndef LMPC_GZ_BMIN
+#define LMPC_GZ_BMIN 0.1
+#endif
+#ifndef LMPC_GZ_BMAX
+#define LMPC_GZ_BMAX 10.0
+#endif
 // one step of iterative refinement of a verified range-space round whose stationarity residual is above
 // LMPC_REFINE_SR of the gradient scale, certified again (round 6); 0: the update as is.  Over 8192 config-2 QPs
 // (tools/refine_diag.py, profiles/r06/refine/) 1857 end on a range-space round; their residuals are <= 6.2e-13 of
@@ -886,10 +905,81 @@ __device__ __forceinline__ bool dense_body(const DevParams prm, const double* __
                 }
             }
 #if LMPC_SPLIT_STEP
+#if LMPC_GONDZIO
+            double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
+            double alpd = fmin(1.0, LMPC_STEP_FRAC * wave_min(dmax));
+#else
             const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(amax));
             const double alpd = fmin(1.0, LMPC_STEP_FRAC * wave_min(dmax));
+#endif
 #else
             const double alpha = fmin(1.0, LMPC_STEP_FRAC * wave_min(fmin(amax, dmax))), alpd = alpha;
+#endif
+#if LMPC_GONDZIO && LMPC_SPLIT_STEP
+            // Gondzio's multiple centrality correctors (diagnostic A/B): while the step is short,
+            // pull the complementarity products of the trial point at a longer step into [bmin, bmax] x sigma mu and
+            // re-solve with the factorisation in hand; keep the new direction if its step is longer by gamma x delta
+            for (int gk = 0; gk < LMPC_GONDZIO; ++gk) {
+                const double am = fmin(alpha, alpd);
+                if (am >= LMPC_GZ_SKIP) break;  // wave-uniform
+                const double tp = fmin(1.0, alpha + LMPC_GZ_DA), td = fmin(1.0, alpd + LMPC_GZ_DA);
+                const double lo = LMPC_GZ_BMIN * smu, hi = LMPC_GZ_BMAX * smu;
+                double rg[5] = {0.0, 0.0, 0.0, 0.0, 0.0}, dsaz[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                double rtg[3] = {0.0, 0.0, 0.0};
+                if (st) {
+                    double oa[5], ua[3], wg[5];
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) ua[m] = S.lua[3 * lane + m];
+                    cons_resid(ua, mu, fzmax, oa);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        const double dsa = -oa[i] - s[i];
+                        const double dza = -z[i] - z[i] * is[i] * dsa;
+                        dsaz[i] = dsa * dza;
+                        const double v = (s[i] + tp * ds[i]) * (z[i] + td * dz[i]);
+                        const double r = v < lo ? lo - v : (v > hi ? fmax(hi - v, -hi) : 0.0);
+                        rg[i] = r;
+                        wg[i] = (z[i] * (s[i] - (i == 4 ? fzmax : 0.0)) + smu + r - dsaz[i]) * is[i];
+                    }
+                    cons_tw(wg, mu, rtg);
+                }
+                LMPC_SYNC();
+                if (st) {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) S.vec[vidx(lane, a)] = -(S.gv[vidx(lane, a)] + rtg[a]);
+                }
+                LMPC_SYNC();
+                solve_vec();
+                double ug[3] = {0.0, 0.0, 0.0}, dsg[5], dzg[5];
+                double amg = 1.0, dmg = 1.0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) dsg[i] = dzg[i] = 0.0;
+                if (st) {
+                    double o[5];
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) ug[a] = S.vec[vidx(lane, a)];
+                    cons_resid(ug, mu, fzmax, o);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        dsg[i] = -o[i] - s[i];
+                        dzg[i] = (smu + rg[i] - z[i] * s[i] - dsaz[i] - z[i] * dsg[i]) * is[i];
+                        if (dsg[i] < 0.0) amg = fmin(amg, -s[i] * __builtin_amdgcn_rcp(dsg[i]));
+                        if (dzg[i] < 0.0) dmg = fmin(dmg, -z[i] * __builtin_amdgcn_rcp(dzg[i]));
+                    }
+                }
+                const double ag = fmin(1.0, LMPC_STEP_FRAC * wave_min(amg));
+                const double adg = fmin(1.0, LMPC_STEP_FRAC * wave_min(dmg));
+                if (!(fmin(ag, adg) >= am + LMPC_GZ_GAMMA * LMPC_GZ_DA)) break;
+                alpha = ag;
+                alpd = adg;
+#pragma unroll
+                for (int m = 0; m < 3; ++m) u[m] = ug[m];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    ds[i] = dsg[i];
+                    dz[i] = dzg[i];
+                }
+            }
 #endif
             if (st) {
 #pragma unroll
