@@ -103,17 +103,17 @@ static void launch_lq_variant(const DevParams& prm, const double* rec, const uin
 // Host-side launcher (lmpc_capi.cpp): cold solves of every QP the dense kernel did not take.  Two waves per SIMD
 // only where the batch has more QPs than the device has SIMDs and more than four fit a CU's LDS (up to one QP per
 // SIMD the lone-wave instance, free of spills, is faster, and the two-wave one would let the dispatcher stack two
-// QPs on one SIMD while others idle).  At two leg-steps per lane (H > 16) the two-wave instance spills 276 B/lane,
-// yet where five or six QPs fit a CU's LDS (H <= 26) the waves it adds hide more than that costs: config 3 (H = 20,
-// 8192 QPs) 3.667 -> 3.454 ms, two alternating runs (round 6, profiles/r06/ls2w2/).  At H = 30 four QPs fill the
-// LDS, so config 5 keeps the lone wave.  Same arithmetic: the choice never changes a result bit.
+// QPs on one SIMD while others idle).  At two leg-steps per lane (H > 16) the two-wave instance spills 276 B/lane:
+// where six or more QPs fit a CU's LDS (H <= 21) the waves it adds hide more than that costs -- config 3 (H = 20,
+// 8192 QPs) 3.667 -> 3.454 ms -- but at five per CU (H = 22..26) it is 8 % slower than the lone wave (round 6,
+// profiles/r06/ls2w2/).  At H = 30 four QPs fill the LDS.  Same arithmetic: the choice never changes a result bit.
 hipError_t launch_lq(const DevParams& prm, const double* rec, const uint8_t* contact, const double* normals, int batch,
                      double* grf, int32_t* status, int32_t* iters, const uint8_t* done, hipStream_t stream) {
     const bool two = 4 * prm.H > 64;
 #ifdef LMPC_AB_NO_W2  // diagnostic variant (tools/ab_bench.sh): the lone-wave instance only
     const bool w2 = false;
 #else
-    const bool w2 = 5 * lq_lds_bytes(prm.H) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
+    const bool w2 = (two ? 6 : 5) * lq_lds_bytes(prm.H) <= LMPC_CU_LDS_BYTES && batch > 4 * prm.cus;
 #endif
 #define LMPC_LQ_LAUNCH(LS_, T_, W_) \
     launch_lq_variant<LS_, T_, W_>(prm, rec, contact, normals, batch, grf, status, iters, done, stream)
