@@ -85,7 +85,10 @@ constexpr int LQF_FIXED = 428;
 // At H <= LQ_KZ_MAXH (one leg-step per lane) the closed-loop rows KZ = K Z (6 x 12 per stage) are kept too, after the
 // slots: the forward sweep is then one 12-term product per row (x' = A x + dv - KZ x - t, t = K za + rho in the rho
 // field) instead of w = Z x + za followed by K w; eight QPs per CU still fit at H = 10.
-constexpr int LQ_KZ_MAXH = 10;
+#ifndef LMPC_LQ_KZ_MAXH  // diagnostic A/B: 0 = no closed-loop rows (a different forward-sweep formula, other bits)
+#define LMPC_LQ_KZ_MAXH 10
+#endif
+constexpr int LQ_KZ_MAXH = LMPC_LQ_KZ_MAXH;
 __host__ __device__ constexpr bool lq_kzs(int H) { return H <= LQ_KZ_MAXH; }
 __host__ __device__ constexpr int lq_lds_doubles(int H) {
     return LQF_FIXED + 2 * H + LQ_SLOT * H + (lq_kzs(H) ? 72 * H : 0);
