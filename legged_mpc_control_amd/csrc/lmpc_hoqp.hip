@@ -771,12 +771,25 @@ __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS
 // Hy y + c + R'z within 1e-9 of the level's scale; otherwise the iterate is kept.  Returns the verdict
 // (uniform); on success S.y holds the exact y.  The reference solves each level exactly with qpOASES
 // (HoQp.cpp:158-174), an active-set method: this makes the degenerate levels exact too.
-constexpr int XO_ROUNDS = 6;
+// Repair rounds (round 6: 12, was 6; profiles/r06/hoqp/): on the 1024 distinct bench chains, with 6 rounds 34
+// level-2 crossovers failed after the first pass (the level resumed the interior point and tried again) and 27
+// levels kept the iterate in the end; with 12, 10 and 7 (9 rounds: 10 kept, 16: 7).  Fewer resumed levels make the
+// 4096-chain launch 2 % faster (4.35 vs 4.44 ms); every golden level verifies either way.
+#ifndef LMPC_HQ_XO_ROUNDS  // -D: diagnostic A/B builds only
+#define LMPC_HQ_XO_ROUNDS 12
+#endif
+constexpr int XO_ROUNDS = LMPC_HQ_XO_ROUNDS;
 constexpr double HQ_HFLOOR = 1e-10;  // interior-point margin on exactly tight frozen rows (kernel, below)
 #ifndef LMPC_HQ_XO_TOL
 #define LMPC_HQ_XO_TOL 1e-9
 #endif
 constexpr double HQ_XO_TOL = LMPC_HQ_XO_TOL;  // first-pass interior-point stop ahead of the crossover (two passes)
+// Diagnostic A/B (tools/build): the first pass also stops after this many iterations (0 = no cap) and hands its
+// iterate to the crossover; a level whose crossover does not verify resumes as after a first-pass stop.
+#ifndef LMPC_HQ_XO_EARLY
+#define LMPC_HQ_XO_EARLY 0
+#endif
+constexpr int HQ_XO_EARLY = LMPC_HQ_XO_EARLY;
 template <int NP>
 __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS& S_, int p, int nr, int nd, double bd0,
                                                     double bd1, int fl0, int fl1, double scale, const gdouble* Hg,
@@ -1098,6 +1111,9 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
         const bool two_pass = P.crossover && P.tol_mu < HQ_XO_TOL;
         bool exact = false;
         int xo = 0;  // iteration word bits 16-17: 1 crossover tried, 2 verified and taken
+#ifdef LMPC_HQ_ITDIAG
+        int it_p0 = 0;
+#endif
         for (int pass = two_pass ? 0 : 1; pass < 2; ++pass) {
             const double tmu = pass == 0 ? HQ_XO_TOL : P.tol_mu;
             for (;; ++it) {
@@ -1144,7 +1160,8 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 // its tolerance while the dual residual stalls within 1e3 of its own, where the huge weights z/s
                 // of those rows leave the Newton directions no more accurate than the iterate already is
                 clean = mu <= tmu * scale && res <= P.tol_res * scale;
-                if (clean || (mu <= 1e-3 * tmu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter)
+                if (clean || (mu <= 1e-3 * tmu * scale && res <= 1e3 * P.tol_res * scale) || it >= P.max_iter ||
+                    (HQ_XO_EARLY > 0 && pass == 0 && it >= HQ_XO_EARLY))
                     break;
                 // weights and K = Hy + R' diag(wh) R
                 double w1[2], wg[2], dl[2], is1[2], isg[2], idl[2];  // weights and the reciprocals both Newton
@@ -1294,6 +1311,9 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
                 xo = exact ? 3 : 1;
                 any_exact = any_exact || exact;
             }
+#ifdef LMPC_HQ_ITDIAG  // diagnostic builds only: the first pass's iteration count in bits 20-27 of the word
+            if (pass == 0) it_p0 = it;
+#endif
             // resume only from a finite iterate that stopped on its criterion (not the cap, not a non-finite direction)
             if (exact || nonfin || numstop || it >= P.max_iter || !(nr > 0 && nd > 0)) break;
         }
@@ -1316,7 +1336,11 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             }
             if (wave_max(viol) > P.tol_res * scale) st = 1;
         }
+#ifdef LMPC_HQ_ITDIAG
+        if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16) | (it_p0 << 20);
+#else
         if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16);
+#endif
         // ---- outputs: w_l = max(0, D_l Z y - g) for the final y, x += Z y ------------------------------
 #pragma unroll
         for (int k = 0; k < 2; ++k) {

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 6: the WBC crossover's repair rounds (LMPC_HQ_XO_ROUNDS 6 = product, 9 / 12 / 16): launch time over the
+# 4096-chain bench batch (two alternating rounds; the bench line's crossover_verified_per_level) and the golden chains.
+export TMPDIR=/tmp
+OUT=gpurun_out/xr
+mkdir -p $OUT
+for r in 1 2; do
+  for tag in prod6 xr9 xr12 xr16; do
+    LMPC_LIB=tools/build/liblmpc_$tag.so timeout -k 10 180 python tools/bench_hoqp.py --steps 20 --warmup 2 --no-cpu \
+      --parity-sample 8 > $OUT/b_${tag}_$r.json 2>/dev/null || exit 3
+    python -c "import json; d=json.load(open('$OUT/b_${tag}_$r.json')); print('$tag', 'kernel_ms %.4f' % d['roofline']['kernel_ms'], d['parity']['final_x_rel_err'], d['crossover_verified_per_level'], d['ipm_iters_per_level_max'])" >> $OUT/ab.log
+  done
+done
+for tag in xr9 xr12 xr16; do
+  echo "== $tag" >> $OUT/xo.log
+  LMPC_LIB=tools/build/liblmpc_$tag.so timeout -k 10 120 python tools/hoqp_xo_check.py >> $OUT/xo.log 2>&1 || exit 4
+  LMPC_LIB=tools/build/liblmpc_$tag.so timeout -k 10 300 python -u -m pytest tests/test_gpu_hoqp.py -x -q -m gpu \
+    --timeout 120 --timeout-method thread > $OUT/tests_$tag.log 2>&1 || echo "$tag tests failed" >> $OUT/xo.log
+done
+cat $OUT/ab.log $OUT/xo.log
