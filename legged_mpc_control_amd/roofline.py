@@ -13,7 +13,7 @@ F0 = 1.544M / 10.72M / 34.44M flop at H = 10 / 20 / 30.
 
 `lq_flop` (the LDS Riccati kernel) and `dense_flop` (the condensed dense interior point) are the useful flops of
 the formulations the kernels run, reported beside it and used as the headline fraction wherever the contract's F0 (a
-dense N = 12H condensation) is not the work done.
+dense N = 12H condensation) is not the work done ("Round 6").
 """
 from __future__ import annotations
 
@@ -28,7 +28,7 @@ HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
 # step against the direct formula, W_j against Bt Rr^-1 Bt') and counts each product as executed (FMA = 2 flops, a
 # lone multiply, division, sqrt or reciprocal 1); the constants are those counts in FMA units (flops / 2).  Round 5's
 # hand tallies were 4 % (factorisations) to 2x (leg-step terms, which multiplied G0_j's structural zeros) higher, in
-# all 13-15 % over the count.  Per horizon stage:
+# all 13-15 % over the count.  Per horizon stage ("Round 6"):
 #   interior-point factorisation (reduced inputs, six unit-cost inputs f = U v - g): U = chol(W), C = P^[:,6:12]
 #     [U | dv], Guu' = I + U'(P22 U), chol(Guu'), X = L^-1 U', K = X'X, P^ dtN, KZ = K Z, dtN' PA, PA' KZ (symmetric)
 #   polish factorisation: the same in reduced inputs where W_k is well conditioned (one leg-step per lane), plus the
