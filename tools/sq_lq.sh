@@ -9,7 +9,7 @@ CFG=${SQ_CFG:---dense off}
 A="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_WAVES"
 B="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU_MFMA_MOPS_F64"
 rc=0
-for path in lds scratch; do
+for path in ${SQ_PATHS:-lds scratch}; do
   for set in A B; do
     C=${!set}
     timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d $OUT/$path$set -o $path$set --output-format csv -- python3 bench.py $CFG --riccati $path --steps 2 --warmup 1 --no-cpu > $OUT/$path$set.log 2>&1 || { rc=$?; break 2; }
