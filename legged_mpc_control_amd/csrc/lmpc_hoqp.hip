@@ -779,6 +779,13 @@ __device__ __attribute__((noinline)) void build_rows(const HoqpDev& P_, const HS
 #define LMPC_HQ_XO_ROUNDS 12
 #endif
 constexpr int XO_ROUNDS = LMPC_HQ_XO_ROUNDS;
+#ifdef LMPC_HQ_ITDIAG  // diagnostic builds only: why the last crossover of a chain failed (bits 28-30 of the word)
+__device__ int lmpc_hq_xo_reason[65536];
+__device__ int lmpc_hq_nnls[65536];  // NNLS calls (low 6 bits) and successes (x 64)
+#define HQ_XO_FAIL(code) do { if (threadIdx.x == 0 && blockIdx.x < 65536) lmpc_hq_xo_reason[blockIdx.x] = (code); } while (0)
+#else
+#define HQ_XO_FAIL(code) do {} while (0)
+#endif
 constexpr double HQ_HFLOOR = 1e-10;  // interior-point margin on exactly tight frozen rows (kernel, below)
 #ifndef LMPC_HQ_XO_TOL
 #define LMPC_HQ_XO_TOL 1e-9
@@ -790,6 +797,111 @@ constexpr double HQ_XO_TOL = LMPC_HQ_XO_TOL;  // first-pass interior-point stop 
 #define LMPC_HQ_XO_EARLY 0
 #endif
 constexpr int HQ_XO_EARLY = LMPC_HQ_XO_EARLY;
+// Multipliers of a degenerate active set (round 6).  Where the active frozen rows are linearly dependent (a foot at
+// the apex of its friction pyramid: four faces tight in three dimensions), the Schur complement R_A T' is singular,
+// its floored LDL' picks one multiplier vector of many and that one can have negative entries although a non-negative
+// one exists; the repair rule then drops a row, the point leaves the vertex, the row re-enters, and the rounds cycle.
+// This finds multipliers lambda >= 0 with R_A' lambda = gr (gr = -(Hy y + c + own rows' terms): the stationarity the
+// verification checks) by Lawson-Hanson NNLS on the active rows (normal equations of the passive set by chol_floor /
+// chol_solve; passive sets of at most na rows, at most 3 na + 3 outer steps).  Returns lambda in lane a (active row
+// S.rt[a]) and whether its residual is within tol.  Uses S.vb, S.KL, S.dI and (through chol_floor) S.dy.
+#ifndef LMPC_HQ_XO_NNLS
+#define LMPC_HQ_XO_NNLS 1
+#endif
+template <int NP>
+__device__ __attribute__((noinline)) double nnls_rows(const HS& S_, int ls, int na, int nd, double gr, double tol,
+                                                      bool& ok, int lane) {
+    const HS S = S_;
+    ls = uni(ls);
+    na = uni(na);
+    nd = uni(nd);
+    const int nt = nd_tiles(nd);
+    const int ra = lane < na ? S.rt[lane] : 0;
+    // R_a' u for lane a (u in S.vb, zero past nd)
+    auto rdot = [&](int r) {
+        double a0 = 0.0, a1 = 0.0;
+        for (int j = 0; j < 16 * nt; j += 2) {
+            a0 = fma(S.R[r * ls + j], S.vb[j], a0);
+            a1 = fma(S.R[r * ls + j + 1], S.vb[j + 1], a1);
+        }
+        return a0 + a1;
+    };
+    // u_j = (R_A' lambda)_j for lane j
+    auto rtl = [&](double lam) {
+        double u = 0.0;
+        for (int a = 0; a < na; ++a) {
+            const double la = readlane_f64(lam, a);
+            if (la != 0.0 && lane < nd) u = fma(la, S.R[uni(S.rt[a]) * ls + lane], u);
+        }
+        return u;
+    };
+    LMPC_SYNC();
+    if (lane < NP) S.vb[lane] = lane < nd ? gr : 0.0;
+    LMPC_SYNC();
+    const double rg = lane < na ? rdot(ra) : 0.0;  // (R_A gr)_a
+    const double eps = 1e-13 * (1.0 + wave_max(fabs(rg)));
+    double lam = 0.0;
+    unsigned long long pas = 0;  // passive set: bit a
+    for (int outer = 0; outer < 3 * na + 3; ++outer) {
+        // w = R_A (gr - R_A' lambda); the most positive w outside the passive set enters
+        const double u = rtl(lam);
+        LMPC_SYNC();
+        if (lane < NP) S.vb[lane] = lane < nd ? u : 0.0;
+        LMPC_SYNC();
+        const bool mem0 = lane < 64 && ((pas >> lane) & 1);
+        const double w = (lane < na && !mem0) ? rg - rdot(ra) : -INFINITY;
+        const double wmax = wave_max(w);
+        if (!(wmax > eps)) break;
+        pas |= 1ull << (__ffsll((long long)__ballot(w == wmax)) - 1);
+        for (int inner = 0; inner <= na && pas; ++inner) {
+            const bool mem = (pas >> lane) & 1;
+            const int m = __popcll(pas);
+            const int pos = __popcll(pas & ((1ull << lane) - 1ull));
+            // the passive rows' Gram matrix into S.KL (row / column = rank in the passive set), zero-padded to whole tiles
+            LMPC_SYNC();
+            unsigned long long rem = pas;
+            int ai = 0;  // lane i < m: the row index a of the i-th passive row
+            for (int col = 0; rem; ++col) {
+                const int b = __ffsll((long long)rem) - 1;
+                rem &= rem - 1;
+                if (col == lane) ai = b;
+                const int rb = uni(S.rt[b]);
+                if (mem) {
+                    double g0 = 0.0, g1 = 0.0;
+                    for (int j = 0; j < 16 * nt; j += 2) {
+                        g0 = fma(S.R[ra * ls + j], S.R[rb * ls + j], g0);
+                        g1 = fma(S.R[ra * ls + j + 1], S.R[rb * ls + j + 1], g1);
+                    }
+                    S.KL[pos * ls + col] = g0 + g1;
+                }
+            }
+            const int nts = nd_tiles(m);
+            if (mem)
+                for (int j = m; j < 16 * nts; ++j) S.KL[pos * ls + j] = 0.0;
+            const double rsh = __shfl(rg, ai);  // every lane takes part: the source lanes must be active
+            const double rhs = lane < m ? rsh : 0.0;
+            LMPC_SYNC();
+            chol_floor<NP>(S, ls, m, lane);
+            const double sv = chol_solve<NP>(S, ls, m, rhs, S.vb, lane);  // lane i: the i-th passive row's value
+            const double sp = __shfl(sv, mem ? pos : 0);
+            const double sa = mem ? sp : 0.0;
+            if (!__any(mem && !(sa > 0.0))) {
+                lam = sa;
+                break;
+            }
+            // move toward the passive solution until the first passive multiplier reaches zero, drop the zeros
+            const double ratio = (mem && !(sa > 0.0) && lam - sa > 0.0) ? lam / (lam - sa) : INFINITY;
+            const double alpha = fmin(1.0, wave_min(ratio));
+            lam = mem ? fma(alpha, sa - lam, lam) : 0.0;
+            pas &= ~__ballot(mem && !(lam > 0.0));
+            lam = ((pas >> lane) & 1) ? lam : 0.0;
+        }
+    }
+    const double u = rtl(lam);
+    ok = wave_max(lane < nd ? fabs(u - gr) : 0.0) <= tol && !__any(lane < na && !(lam >= 0.0));
+    return lam;
+}
+
 template <int NP>
 __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS& S_, int p, int nr, int nd, double bd0,
                                                     double bd1, int fl0, int fl1, double scale, const gdouble* Hg,
@@ -837,7 +949,7 @@ __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS&
         if (lane < np) S.dy[lane] = y0;
         const unsigned long long m0 = __ballot(fl[0] & 1), m1 = __ballot(fl[1] & 1);
         const int na = __popcll(m0) + __popcll(m1);
-        if (na > np || na > 64) return false;
+        if (na > np || na > 64) { HQ_XO_FAIL(1); return false; }
         LMPC_SYNC();
         // T rows a = K_A^-1 R_{r_a}' (global scratch); active row indices in S.rt
         unsigned long long w0 = m0, w1 = m1;
@@ -899,17 +1011,46 @@ __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS&
             LMPC_SYNC();
             chol_floor<NP>(S, ls, na, lane);
             lam = chol_solve<NP>(S, ls, na, e, S.vb, lane);  // lane a: lambda_a
+            const bool degen = __any(lane < na && S.dI[lane] < 1e-60);  // a floored pivot: dependent active rows
             for (int a = 0; a < na; ++a) {
                 const double la = readlane_f64(lam, a);
                 if (lane < nd) y = fma(-la, Tg[(int64_t)a * np + lane], y);
             }
             if (lane < np) S.dy[lane] = lane < nd ? y : 0.0;
             LMPC_SYNC();
+#if LMPC_HQ_XO_NNLS
+            // dependent active rows with a negative multiplier: non-negative multipliers for the same point, if some
+            // exist (nnls_rows); the point y is the one above either way
+            // (only where the point meets every active row: dependent rows whose bounds disagree have no such point)
+            double ares = 0.0;
+            if (degen && lane < na) {
+                const int rb = S.rt[lane];
+                ares = fabs(row_dot<NP>(S, ls, nd, rb, S.dy) - S.t[rb]);
+            }
+            if (degen && wave_min(lane < na ? lam : INFINITY) < -tol && wave_max(ares) <= tol) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int r = lane + 64 * k;
+                    if (r < P.rmax) S.q[r] = (r < nr && r >= p && (fl[k] & 2)) ? row_dot<NP>(S, ls, nd, r, S.dy) - bd[k] : 0.0;
+                }
+                LMPC_SYNC();
+                const double gr = lane < nd ? -(hy_dot<NP>(P, Hg, S.dy, nd, lane) + S.c[lane] + rt_dot(S, ls, nr, S.q, lane)) : 0.0;
+                bool ok = false;
+                const double ln = nnls_rows<NP>(S, ls, na, nd, gr, tol, ok, lane);
+#ifdef LMPC_HQ_ITDIAG
+                if (lane == 0 && blockIdx.x < 65536) lmpc_hq_nnls[blockIdx.x] += ok ? 65 : 1;
+#endif
+                if (lane < np) S.dy[lane] = lane < nd ? y : 0.0;  // chol_floor's column buffer
+                LMPC_SYNC();
+                if (ok) lam = ln;
+            }
+#endif
         }
         // verification, and the repair of the classification
         double t[2];
         bool flip = false;
         double vin = -INFINITY;  // most violated inactive frozen row
+        bool abad = false;       // an active frozen row the point does not meet (dependent rows with disagreeing bounds)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int r = lane + 64 * k;
@@ -918,6 +1059,7 @@ __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS&
                 t[k] = row_dot<NP>(S, ls, nd, r, S.dy) - bd[k];
                 if (r < p) {
                     if (!(fl[k] & 1)) vin = fmax(vin, t[k]);
+                    else abad |= !(fabs(t[k]) <= tol);
                 } else {
                     const bool fk = (fl[k] & 2) ? !(t[k] >= -tol) : !(t[k] <= tol);
                     flip |= fk;
@@ -927,7 +1069,7 @@ __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS&
         const double lmin = wave_min(lane < na ? lam : INFINITY);
         const double vmax = wave_max(vin);
         const bool anyflip = __any(flip);
-        if (!(lmin == lmin) || !(vmax == vmax)) return false;  // non-finite
+        if (!(lmin == lmin) || !(vmax == vmax)) { HQ_XO_FAIL(2); return false; }  // non-finite
         bool changed = false;
         if (lmin < -tol) {  // the most negative multiplier's row leaves the active set
             const int a = __ffsll((long long)__ballot(lane < na && lam == lmin)) - 1;
@@ -958,6 +1100,10 @@ __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS&
             changed = true;
         }
         if (changed) continue;
+        if (__any(abad)) {
+            HQ_XO_FAIL(5);
+            return false;
+        }
         // stationarity: Hy y + c + R'z, z = lambda on the active frozen rows, R y - g on the violated own rows
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -969,11 +1115,13 @@ __device__ __attribute__((noinline)) bool crossover(const HoqpDev& P_, const HS&
         LMPC_SYNC();
         double st = 0.0;
         if (lane < nd) st = hy_dot<NP>(P, Hg, S.dy, nd, lane) + S.c[lane] + rt_dot(S, ls, nr, S.q, lane);
-        if (__any(!(fabs(st) <= tol) || !(y == y))) return false;  // NaN fails every comparison
+        if (__any(!(fabs(st) <= tol) || !(y == y))) { HQ_XO_FAIL(3); return false; }  // NaN fails every comparison
         if (lane < np) S.y[lane] = lane < nd ? y : 0.0;
         LMPC_SYNC();
+        HQ_XO_FAIL(0);
         return true;
     }
+    HQ_XO_FAIL(4);
     return false;
 }
 
@@ -1337,7 +1485,9 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
             if (wave_max(viol) > P.tol_res * scale) st = 1;
         }
 #ifdef LMPC_HQ_ITDIAG
-        if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16) | (it_p0 << 20);
+        const int xr = (xo & 1) ? lmpc_hq_xo_reason[b < 65536 ? b : 0] : 0;
+        if (lane == 0 && iters && b < 65536 && l == P.L - 1) lmpc_hq_xo_reason[b] = lmpc_hq_nnls[b];
+        if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16) | (it_p0 << 20) | (xr << 28);
 #else
         if (iters && lane == 0) iters[(int64_t)b * P.L + l] = it | (xo << 16);
 #endif
@@ -1407,6 +1557,12 @@ __global__ void __launch_bounds__(64) lmpc_hoqp_kernel(const HoqpDev P, const do
     if (status && lane == 0) status[b] = st;
 }
 
+#ifdef LMPC_HQ_ITDIAG
+extern "C" int lmpc_debug_hoqp_nnls(int* out, int n) {
+    if (n > 65536) n = 65536;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lmpc_hq_nnls), (size_t)n * sizeof(int)) == hipSuccess ? n : -1;
+}
+#endif
 #ifdef LMPC_STAMPS
 extern "C" int lmpc_debug_hoqp_stamps(unsigned long long* out, int n) {
     if (n > 4096) n = 4096;

@@ -172,6 +172,23 @@ def test_wbc_batch_properties_at_scale(hq):
     assert np.all(w >= 0.0)
 
 
+def test_every_bench_level_verifies_exactly(hq):
+    """Round 6: the crossover of every level of the bench's 1024 distinct WBC chains verifies (iteration word bits
+    16-17 = 3: an exact active-set answer, no interior-point iterate kept).  Before round 6, 27 level-2 crossovers ran
+    out of repair rounds: dependent active rows (a foot at the apex of its friction pyramid) gave a negative
+    multiplier, the repair dropped the row, the point left the vertex and the row came back.  With 12 rounds 7 still
+    cycled; the non-negative multipliers of such sets (nnls_rows, lmpc_hoqp.hip) verify them all."""
+    from legged_mpc_control_amd import wbc as W
+
+    chains = [W.synth_wbc_tasks(1_000_000 + i) for i in range(1024)]  # tools/bench_hoqp.py's instances
+    dims = hq.dims_of(chains[0])
+    rec = np.ascontiguousarray(np.stack([hq.pack(c, dims) for c in chains]))
+    x, w, st, it = hq.HoqpBatch(dims, rec.shape[0]).solve(rec)
+    assert np.all(st == 0)
+    xo = (it >> 16) & 3
+    assert np.all(xo == 3), f"levels not verified: {np.argwhere(xo != 3)[:10].tolist()}"
+
+
 def test_level_without_equalities(hq):
     """A level with only inequality rows (the reference hands qpOASES a zero Hessian block there; here the
     1e-12 term): runs, converges, keeps the higher level's equality values and meets its own rows."""

@@ -32,6 +32,7 @@ def main():
     it = word & 0xFFFF
     xo = (word >> 16) & 3
     it0 = (word >> 20) & 0xFF
+    why = (word >> 28) & 7  # the last crossover's failure: 1 too many active rows, 2 non-finite, 3 stationarity, 4 rounds
     print("status", np.bincount(st, minlength=3))
     for l in range(it.shape[1]):
         res = it[:, l] > it0[:, l]
@@ -39,6 +40,8 @@ def main():
               f"{it0[:, l].mean():.2f} max {it0[:, l].max()}; resumed {res.sum()} (their total iterations "
               f"{np.bincount(it[res, l]).nonzero()[0].tolist()}); crossover bits {np.bincount(xo[:, l], minlength=4)}")
         print("   first-pass histogram", np.bincount(it0[:, l]).tolist())
+        print("   last crossover's failure reason (levels not verified: 1 rows, 2 non-finite, 3 stationarity, 4 rounds)",
+              np.bincount(why[xo[:, l] == 1, l], minlength=5).tolist())
         print("   total histogram     ", np.bincount(it[:, l]).tolist())
     tot = it.sum(1)
     print(f"iterations per chain: mean {tot.mean():.2f} p99 {np.percentile(tot, 99):.0f} max {tot.max()}")
@@ -64,6 +67,15 @@ def main():
                 free[k] += v
             print(f"  {tile} chains on {slots} slots, index order: makespan {free.max():.0f} cycles = "
                   f"{free.max() / (c.sum() / slots):.3f} x the mean load")
+    if hasattr(L, "lmpc_debug_hoqp_nnls"):  # NNLS calls / successes per chain (cumulative over launches)
+        import ctypes
+        L.lmpc_debug_hoqp_nnls.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        nb = np.zeros(nd, dtype=np.int32)
+        L.lmpc_debug_hoqp_nnls(nb.ctypes.data, nd)
+        calls, succ = nb % 64, nb // 64
+        print(f"NNLS: chains calling it {int((calls > 0).sum())}, calls {int(calls.sum())}, successes {int(succ.sum())}")
+        unver = np.nonzero((xo == 1).any(1))[0]
+        print("  unverified chains:", [(int(b), int(calls[b]), int(succ[b])) for b in unver])
     order = np.argsort(-(cyc if cyc is not None else tot))
     for b in order[:12]:
         extra = f" {cyc[b]:.0f} cycles" if cyc is not None else ""
