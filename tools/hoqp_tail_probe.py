@@ -32,7 +32,7 @@ def main():
     it = word & 0xFFFF
     xo = (word >> 16) & 3
     it0 = (word >> 20) & 0xFF
-    why = (word >> 28) & 7  # the last crossover's failure: 1 too many active rows, 2 non-finite, 3 stationarity, 4 rounds
+    why = (word >> 28) & 7  # the last crossover's failure: 1 too many active rows, 2 non-finite, 3 stationarity, 4 rounds, 5 an active row not met
     print("status", np.bincount(st, minlength=3))
     for l in range(it.shape[1]):
         res = it[:, l] > it0[:, l]
@@ -40,8 +40,8 @@ def main():
               f"{it0[:, l].mean():.2f} max {it0[:, l].max()}; resumed {res.sum()} (their total iterations "
               f"{np.bincount(it[res, l]).nonzero()[0].tolist()}); crossover bits {np.bincount(xo[:, l], minlength=4)}")
         print("   first-pass histogram", np.bincount(it0[:, l]).tolist())
-        print("   last crossover's failure reason (levels not verified: 1 rows, 2 non-finite, 3 stationarity, 4 rounds)",
-              np.bincount(why[xo[:, l] == 1, l], minlength=5).tolist())
+        print("   last crossover's failure reason (levels not verified: 1 rows, 2 non-finite, 3 stationarity, 4 rounds, 5 active row not met)",
+              np.bincount(why[xo[:, l] == 1, l], minlength=6).tolist())
         print("   total histogram     ", np.bincount(it[:, l]).tolist())
     tot = it.sum(1)
     print(f"iterations per chain: mean {tot.mean():.2f} p99 {np.percentile(tot, 99):.0f} max {tot.max()}")
