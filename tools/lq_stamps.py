@@ -29,6 +29,8 @@ calls = {0: np.ones(n), 1: 2 * ipm + rnd, 2: ipm, 3: ipm + rnd, 4: 2 * ipm + rnd
 names = ["prologue", "leg-step work", "corr backward", "factorisation", "forward sweep", "inputs", "pred step",
          "corr step", "adjoint", "polish check", "epilogue", " f:C,PA,G", " f:leg blocks", " f:KH", " f:KZ,P", " f:polish (incl.)"]
 tot = buf[:, :15].sum(1)
+if os.environ.get("LQ_STAMPS_DUMP"):  # per-QP cycles and iteration words, for a cost-predictor study on the CPU
+    np.savez(os.environ["LQ_STAMPS_DUMP"], cycles=tot, it=it[:n], config=cid, count=count)
 print(f"LDS kernel: config {cid} H={H} B={count}: mean cycles/QP {tot.mean():.0f} max {tot.max():.0f}  "
       f"ipm {ipm.mean():.2f} rounds {rnd.mean():.2f}")
 for i, nm in enumerate(names):
