@@ -171,7 +171,7 @@ def level_ipm(Hy, c, P, h, Dz, g, max_iter=60, tol=float(os.environ.get('TOL', 1
     m = 2 * s + p
     init = os.environ.get("INIT", "zero")
     y = np.zeros(nd)
-    if init.startswith("ls"):  # unconstrained minimiser of the level objective
+    if init == "ls" or (init == "ls0" and p == 0):  # unconstrained minimiser of the level objective (ls0: level 0)
         y = chol_solve(chol_floor(Hy), -c)
     floor = float(os.environ.get("SFLOOR", 1.0))
     v = np.maximum(0.0, (Dz @ y - g) if s else 0.0) + floor if s else np.zeros(0)
