@@ -111,7 +111,7 @@ typedef struct lmpc_options {
     int max_rounds;   /* active-set polish rounds per attempt (default 8) */
     int max_attempts; /* IPM+polish attempts (default 3); each retry stops the IPM 1e-3 tighter, at most
                          1e-8 on the second attempt and 1e-12 on the third (1e-4 lower each further one) */
-    double tol_mu;    /* IPM stop: mean complementarity, then the polish (default 1e-4) */
+    double tol_mu;    /* IPM stop: mean complementarity, then the polish (default 2e-4; 1e-4 until round 6) */
     double tol_p;     /* polish primal feasibility, relative to f_max (default 1e-9) */
     double tol_d;     /* polish multiplier sign, relative to gradient scale (default 1e-9) */
     /* ABI 5: the dense paths' caps and the warm-start budget (were environment hooks).  None of them
